@@ -1,0 +1,199 @@
+"""Throughput benchmark: env-steps/s of the batched CraftWorld on MI355X.
+
+One "step" = one rollout tick of every env on every GPU (craft_step: the
+do_rollout body + step() + satisfies() + the full features() observation,
+auto-reset), i.e. BASELINE.json's metric on 12x12 craft_medium with 65536 envs
+per GPU (configs[2]; configs[3] is the 8-GPU sharding of the same).  Inputs
+(scenario pool, env states) are resident in HBM before the timed region;
+observations stream into a ring of R device buffers (R * 106 MB > the 256 MB
+Infinity Cache) as a trainer's per-tick feature tensors would.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Rank 0 prints one JSON line (see the contract in the task description).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def bytes_per_env_step(W, H, window, F):
+    """Algorithmic HBM bytes per env-step: 57 B of step state
+    (action 1 + agent state r/w 48 + facing/target cells 2 + cell write 1 +
+    reward 4 + done 1) + the fp32 observation row F*4 + the pooled window's
+    grid cells min(w^2, W) * min(w^2, H)."""
+    ww = window * window
+    return 57 + 4 * F + min(ww, W) * min(ww, H)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    p.add_argument("--world", default="craft_medium_12x12")
+    p.add_argument("--pool", type=int, default=1024)
+    p.add_argument("--ring", type=int, default=4, help="observation buffers cycled per tick")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(sim, grids, specs, seconds):
+    """The CPU oracle (C restatement, 1 thread) on a bounded sample of the same
+    workload; env-steps/s."""
+    import oracle
+    n = 4096
+    o = oracle.Oracle(sim.config, grids)
+    envs = o.init_envs(*[a[:n] for a in specs])
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        steps += o.bench(envs, 20, seed=1)
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} envs x {steps // n} ticks ({dt:.1f} s) of the same workload "
+                      "(12x12 craft_medium, hashed actions, auto-reset): step + satisfies + "
+                      "full features() per env-step, oracle/craft_oracle.c, 1 thread"}
+
+
+def main():
+    args = parse()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world_size > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
+
+    n = args.envs
+    sim = CraftSim(args.world, n_envs=n, device=local_rank, env_id_base=rank * n,
+                   pool_capacity=args.pool)
+    grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
+    sim.load_pool(grids)
+    tasks = [t.id for t in sim.task_manager.dataset_tasks()]
+    specs = synthetic_specs(grids, sim.width, sim.height, n, rank * n, seed=args.seed,
+                            task_ids=tasks)
+    sim.reset(*specs)
+    F = sim.n_features
+    ring = [sim.empty_obs() for _ in range(args.ring)]
+    reward = torch.empty(n, dtype=torch.float32, device=dev)
+    done = torch.empty(n, dtype=torch.uint8, device=dev)
+    success = torch.empty(n, dtype=torch.int8, device=dev)
+
+    tick = 0
+
+    def step():
+        nonlocal tick
+        sim.step(seed=args.seed, tick=tick, obs=ring[tick % args.ring], reward=reward, done=done,
+                 success=success)
+        tick += 1
+
+    for _ in range(args.warmup):
+        step()
+    sim.check()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---- timed region: K ticks, barrier + synchronize on both sides ------------------
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # ---- per-launch kernel duration, HIP events on the launch stream --------------------
+    kstream = torch.cuda.current_stream(dev)
+    m = min(args.steps, 400)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(m)]
+    torch.cuda.synchronize()
+    for a, b in evs:
+        a.record(kstream)
+        step()
+        b.record(kstream)
+    torch.cuda.synchronize()
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    # ---- scalar episode summary: one RCCL all-reduce of int64[3] --------------------------
+    stats = sim.stats()
+    if dist is not None:
+        dist.all_reduce(stats)
+    stats = stats.cpu().tolist()
+    sim.check()
+
+    if rank == 0:
+        total_steps = n * world_size * args.steps
+        value = total_steps / elapsed
+        bps = bytes_per_env_step(sim.width, sim.height, sim.params["WINDOW_WIDTH"], F)
+        achieved = bps * n / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        workload = f"{args.world}_w{sim.params['WINDOW_WIDTH']}_B{n}_random_rollout_full_features"
+        if os.path.exists(args.traffic):
+            try:
+                tj = json.load(open(args.traffic))
+                if tj.get("workload") == workload:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: 1024 make_data.sample_scenario worlds (RandomState(123)), "
+                    "per-env init keyed by global id, splitmix64 actions",
+            "config": {"workload": workload, "world": args.world, "envs_per_gpu": n,
+                       "global_batch": n * world_size, "window": sim.params["WINDOW_WIDTH"],
+                       "n_features": F, "obs_dtype": "fp32", "obs_ring": args.ring,
+                       "pool": args.pool, "parallelism": f"env-shard x{world_size}",
+                       "max_timesteps": sim.config.max_timesteps},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "tile_kernel<3, MODE_TICK>",
+                         "kernel_us": kernel_ms * 1e3, "bytes_per_env_step": bps},
+            "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},
+        }
+        if world_size == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(sim, grids, specs, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

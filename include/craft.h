@@ -1,0 +1,251 @@
+/*
+ * craft.h — C ABI of the MI355X-native batched CraftWorld simulator.
+ *
+ * The reference (khanhptnk/psketch) has no FFI: its boundary is the Python
+ * duck-typed world protocol selected by name in worlds/__init__.py:5-11
+ * (`globals()[config.world.name](config)`).  Every entry point below replaces
+ * one piece of that protocol, batched over N environments that live as
+ * struct-of-arrays in HBM.  The Python host side (psketch_amd/) binds these
+ * with ctypes; INTEGRATION.md shows the binding a maintainer adds to the
+ * reference.
+ *
+ * Conventions
+ *   - Plain C types only.  `stream` is a hipStream_t passed as void* (NULL =
+ *     the null stream).  Pointers documented "device" are HBM pointers owned by
+ *     the caller; "host" pointers are host memory owned by the caller.
+ *   - Every function returns a craft_status (0 = CRAFT_OK).  A failing call
+ *     stores a message retrievable with craft_sim_last_error().
+ *   - Kernel-side errors (an out-of-range action, a teacher assertion) cannot
+ *     be returned synchronously; they latch in a device error word that
+ *     craft_sim_check() reads (it synchronises the stream).
+ *   - A handle is not thread-safe; calls are stream-ordered.  No allocation
+ *     happens on the step path.
+ *
+ * Grid convention: cell (x, y) of a W x H world is index x*H + y (x-major),
+ * exactly the order of `grid[x, y, :]` in worlds/craft.py and of
+ * `np.nonzero` in CraftState.find_resource_positions (craft.py:453-455).
+ * A cell holds one kind id (0 = empty); the reference's one-hot W x H x K
+ * float64 grid maps 1:1 onto it (its one-kind-per-cell invariant is asserted
+ * at craft.py:365-371 and checked when a grid is loaded).
+ */
+#ifndef PSKETCH_CRAFT_H
+#define PSKETCH_CRAFT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRAFT_ABI_VERSION 1
+
+#define CRAFT_MAX_KINDS 32       /* len(cookbook.index) incl. reserved 0 (21 for recipes.yaml) */
+#define CRAFT_MAX_RECIPES 16     /* recipes.yaml has 9 */
+#define CRAFT_MAX_INGREDIENTS 4
+#define CRAFT_MAX_TASKS 64       /* hints.hierarchy.yaml has 26 */
+#define CRAFT_MAX_SUBTASKS 4
+#define CRAFT_MAX_DIM 16         /* W, H <= 16 */
+#define CRAFT_MAX_CELLS 256      /* W * H <= 256 */
+
+/* status codes */
+typedef enum craft_status {
+  CRAFT_OK = 0,
+  CRAFT_EINVAL = 1,       /* bad argument / configuration */
+  CRAFT_EBADACTION = 2,   /* action outside 0..5: craft.py:415-416 `Exception("Unexpected action")` */
+  CRAFT_EINVARIANT = 3,   /* grid breaks an invariant: craft.py:365-371 AssertionError */
+  CRAFT_ETEACHER = 4,     /* teacher assertion / crash: teachers/base.py:24,31; demonstration.py:18 */
+  CRAFT_EHIP = 5,         /* HIP runtime failure */
+  CRAFT_ENOMEM = 6,
+  CRAFT_ERANGE = 7        /* slot / scenario index out of range */
+} craft_status;
+
+/* Actions, craft.py:25-31.  Moves use world.actions.*.coord_change, craft.py:77-91. */
+enum {
+  CRAFT_DOWN = 0,   /* (0, -1) */
+  CRAFT_UP = 1,     /* (0, +1) */
+  CRAFT_LEFT = 2,   /* (-1, 0) */
+  CRAFT_RIGHT = 3,  /* (+1, 0) */
+  CRAFT_USE = 4,
+  CRAFT_STOP = 5,
+  CRAFT_N_ACTIONS = 6
+};
+
+/* What USE does to a facing cell holding a kind (craft.py:373-410, 101-107). */
+enum {
+  CRAFT_KIND_INERT = 0,      /* boundary, or a workshop index >= N_WORKSHOPS: USE is a no-op */
+  CRAFT_KIND_GRABBABLE = 1,  /* not in cookbook.environment: inventory += 1, cell cleared */
+  CRAFT_KIND_WORKSHOP = 2,   /* workshop0..N_WORKSHOPS-1: apply its recipes in dict order */
+  CRAFT_KIND_WATER = 3,      /* with bridge > 0: cell cleared, bridge -= 1 */
+  CRAFT_KIND_STONE = 4       /* with axe > 0: cell cleared, axe kept */
+};
+
+/* Task.goal_name values (data/task.py:11) that CraftState.satisfies and the
+ * DemonstrationTeacher distinguish (craft.py:285-294, teachers/demonstration.py:18-21). */
+enum {
+  CRAFT_GOAL_OTHER = 0,   /* left/right/up/down/stop/makeat: satisfies() -> None */
+  CRAFT_GOAL_GET = 1,     /* inventory[arg] > 0 */
+  CRAFT_GOAL_MAKE = 2,    /* inventory[arg] > 0 */
+  CRAFT_GOAL_GO = 3,      /* facing cell holds arg */
+  CRAFT_GOAL_USE = 4      /* satisfies() -> None; teacher leaf -> USE */
+};
+
+typedef struct craft_recipe {
+  int32_t output;        /* kind id produced */
+  int32_t workshop;      /* kind id of its `_at` workshop */
+  int32_t yield;         /* `_yield`, default 1 (craft.py:394) */
+  int32_t n_inputs;
+  int32_t input_kind[CRAFT_MAX_INGREDIENTS];
+  int32_t input_count[CRAFT_MAX_INGREDIENTS];
+} craft_recipe_t;
+
+typedef struct craft_task {
+  int32_t goal;          /* CRAFT_GOAL_* */
+  int32_t arg_kind;      /* cookbook.index[goal_arg]; 0 when the arg is not a kind */
+  int32_t n_subtasks;    /* 0 = leaf (data/task.py:13-15) */
+  int32_t subtask[CRAFT_MAX_SUBTASKS];   /* task ids, in hint order */
+} craft_task_t;
+
+/* Static world tables: CraftWorld.__init__ (craft.py:59-109), Cookbook
+ * (worlds/cookbook.py:8-26), TaskManager (data/task.py:32-75). */
+typedef struct craft_config {
+  int32_t abi_version;       /* = CRAFT_ABI_VERSION */
+  int32_t width, height;     /* WIDTH, HEIGHT */
+  int32_t window_width, window_height;   /* WINDOW_WIDTH, WINDOW_HEIGHT (odd, equal, 3..7) */
+  int32_t n_kinds;           /* len(cookbook.index) */
+  int32_t n_features;        /* must equal 2*ww*wh*n_kinds + n_kinds + 5 (craft.py:69-75) */
+  int32_t max_timesteps;     /* trainer.max_timesteps (configs/experiments/imitation.yaml:21) */
+  int32_t bridge_kind, axe_kind;
+  uint8_t kind_class[CRAFT_MAX_KINDS];   /* CRAFT_KIND_* per kind id */
+  int32_t n_recipes;
+  craft_recipe_t recipe[CRAFT_MAX_RECIPES];   /* cookbook.recipes in dict (YAML) order */
+  int32_t n_tasks;
+  craft_task_t task[CRAFT_MAX_TASKS];         /* TaskManager.tasks order */
+} craft_config_t;
+
+typedef struct craft_sim craft_sim_t;
+
+/* ---- handle lifetime ------------------------------------------------------ */
+
+/* Replaces CraftWorld.__init__ (craft.py:59-109) for a batch of `n_envs`
+ * environment slots on `device`.  `env_id_base` is the global id of slot 0
+ * (rank * n_envs when sharded): per-env randomness is keyed by global id so
+ * results do not depend on the number of GPUs.  `pool_capacity` scenario
+ * grids can be loaded. */
+int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs,
+                     int64_t env_id_base, int32_t pool_capacity, craft_sim_t** out);
+int craft_sim_destroy(craft_sim_t* sim);
+const char* craft_sim_last_error(const craft_sim_t* sim);
+const char* craft_strerror(int status);
+int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capacity,
+                   int32_t* n_features);
+
+/* Synchronises `stream` and returns the first kernel-side error latched since
+ * the last call (then clears it); *env_out receives the offending slot. */
+int craft_sim_check(craft_sim_t* sim, int64_t* env_out, void* stream);
+
+/* ---- scenario pool ---------------------------------------------------------- */
+
+/* Uploads `count` initial grids (host, count * W*H kind ids, x-major) into pool
+ * entries [first, first+count).  Replaces the `grid` handed to
+ * CraftWorld.init_state (craft.py:258-259).  Rejects kind ids >= n_kinds and
+ * worlds whose border ring is not fully occupied (every make_data.py world has
+ * the boundary ring, make_data.py:108-112). Synchronous. */
+int craft_pool_load(craft_sim_t* sim, const uint8_t* grids, int32_t first, int32_t count);
+
+/* ---- episodes ---------------------------------------------------------------- */
+
+/* CraftScenario.init (craft.py:262-273) for every slot: inventory zeroed,
+ * grid = pool[scenario], pos/dir given, timer = max_timesteps.  The spec is
+ * kept so that an auto-reset returns the slot to the same initial state.
+ * Device arrays of n_envs int32 each; `obs` (n_envs x n_features fp32) may be
+ * NULL, else receives features() of the initial states. */
+int craft_reset(craft_sim_t* sim, const int32_t* scenario, const int32_t* pos_x,
+                const int32_t* pos_y, const int32_t* dir, const int32_t* task,
+                float* obs, void* stream);
+
+#define CRAFT_STEP_AUTORESET 1u   /* done slots restart from their spec next tick */
+
+/* One tick of the imitation-trainer rollout for every slot, fused with the
+ * observation: the per-env body of ImitationTrainer.do_rollout
+ * (trainers/imitation.py:59-73) followed by CraftState.features() of the new
+ * state (craft.py:296-330).
+ *   timer -= 1; done = (a == STOP) or timer <= 0
+ *   done  -> success = satisfies(task) on the pre-step state, no step
+ *            (auto-reset: the slot restarts; else it stays frozen)
+ *   !done -> state = step(state, a)            (craft.py:332-424)
+ * `actions` (device int32[n_envs]) may be NULL: actions are then drawn in the
+ * kernel as splitmix64(action_seed ^ (gid << 20) ^ tick) >> 32 mod 6.
+ * Outputs (device, each may be NULL): obs fp32[n_envs][n_features];
+ * reward fp32 (1 on a tick that ends an episode with satisfies() true, else 0 —
+ * step() itself always returns 0, craft.py:338); done uint8; success int8
+ * (-1 not terminal, else satisfies()).  Episode statistics accumulate inside
+ * the handle (per-workgroup partial sums, no atomics); read them with
+ * craft_stats. */
+int craft_step(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed, int64_t tick,
+               uint32_t flags, float* obs, float* reward, uint8_t* done, int8_t* success,
+               void* stream);
+
+/* Sums the episode statistics accumulated by craft_step into stats_out
+ * (device int64[3] = {successes, episodes ended, env-steps}) — the scalar
+ * summary a multi-GPU run all-reduces over RCCL.  reset != 0 zeroes the
+ * partial sums afterwards. */
+int craft_stats(craft_sim_t* sim, int64_t* stats_out, int32_t reset, void* stream);
+
+/* ---- reference-granular surface (CraftState methods), over slot lists ---- */
+
+/* CraftState.step (craft.py:332-424) as a pure transition: slot dst[i] becomes
+ * step(slot src[i], actions[i]) — src == dst updates in place, src != dst keeps
+ * the old state (the reference's states are immutable).  actions[i] < 0 is a
+ * no-op copy.  src/dst NULL = identity over n slots.  Device int32 arrays. */
+int craft_transition(craft_sim_t* sim, const int32_t* src, const int32_t* dst,
+                     const int32_t* actions, int64_t n, void* stream);
+
+/* CraftState.features() (craft.py:296-330) and satisfies() (craft.py:285-294)
+ * for n slots (NULL = identity).  obs: fp32[n][n_features] or NULL; sat: int8[n]
+ * (-1 = None, 0/1) for task tasks[i] (NULL = the slot's own task) or NULL. */
+int craft_observe(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* tasks,
+                  float* obs, int8_t* sat, void* stream);
+
+/* DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for n slots:
+ * find_incomplete_subtask over the hint tree then the BFS of
+ * find_closest_resources/shortest_path (teachers/base.py:10-87).
+ * action_out int32[n]; path_len_out int32[n] (may be NULL) receives
+ * len(best_action_seq) of find_closest_resources for the task's own goal_arg
+ * (the trainer's `distances`, trainers/imitation.py:79-91), -1 if no target.
+ * Where the reference raises (base.py:24 assert, base.py:31 len(None),
+ * demonstration.py:18 assert) the item gets -2 and CRAFT_ETEACHER latches. */
+int craft_teacher(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* tasks,
+                  int32_t* action_out, int32_t* path_len_out, void* stream);
+
+/* State I/O for the Python CraftState shim and for parity tests (device
+ * arrays, n slots, NULL slot list = identity).  grid: uint8[n][W*H] current
+ * kind ids; inventory: int32[n][n_kinds]; agent: int32[n][4] = {x, y, dir, timer};
+ * spec: int32[n][5] = {scenario, x0, y0, dir0, task}. */
+int craft_get_state(craft_sim_t* sim, const int32_t* slots, int64_t n, int32_t* agent,
+                    int32_t* inventory, uint8_t* grid, int32_t* spec, void* stream);
+/* Sets slots to (scenario grid with no removals, agent, inventory); spec as above. */
+int craft_set_state(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* spec,
+                    const int32_t* agent, const int32_t* inventory, void* stream);
+
+/* ---- host-side scenario generation ------------------------------------------ */
+
+/* make_data.sample_scenario (make_data.py:105-144) with `random_free`
+ * (make_data.py:74-103) and `all_free_cells_reachable` (make_data.py:27-72),
+ * drawing from numpy's legacy RandomState(seed) MT19937 stream bit-exactly.
+ * Generates `count` scenarios (each rejected and redrawn while it duplicates an
+ * earlier one when `dedup`, make_data.py:167-177).  grids_out: host
+ * uint8[count][W*H]; init_pos_out: host int32[count][2].  `primitives` lists the
+ * primitive kind ids in the iteration order of cookbook.primitives with gold/gem
+ * already removed (make_data.py:128-134); workshops are kinds workshop_kind[0..n_ws).
+ * The MT19937 state after the last draw is written to mt_state_out (625 uint32,
+ * may be NULL) so a caller can continue numpy's stream. */
+int craft_sample_scenarios(int32_t width, int32_t height, int32_t boundary_kind,
+                           const int32_t* primitives, int32_t n_primitive_kinds,
+                           int32_t n_per_primitive, const int32_t* workshop_kind,
+                           int32_t n_workshops, uint32_t seed, int32_t count, int32_t dedup,
+                           uint8_t* grids_out, int32_t* init_pos_out, uint32_t* mt_state_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSKETCH_CRAFT_H */

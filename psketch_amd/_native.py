@@ -1,0 +1,141 @@
+"""ctypes binding of the C ABI in include/craft.h (libpsketch_craft.so).
+
+The library is the product: every simulator call goes through it and there is
+no CPU fallback.  Importing this module without the built library raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first so the library shares it)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpsketch_craft.so")
+
+ABI_VERSION = 1
+MAX_KINDS = 32
+MAX_RECIPES = 16
+MAX_INGREDIENTS = 4
+MAX_TASKS = 64
+MAX_SUBTASKS = 4
+MAX_DIM = 16
+MAX_CELLS = 256
+
+OK, EINVAL, EBADACTION, EINVARIANT, ETEACHER, EHIP, ENOMEM, ERANGE = range(8)
+
+DOWN, UP, LEFT, RIGHT, USE, STOP = range(6)
+N_ACTIONS = 6
+
+KIND_INERT, KIND_GRABBABLE, KIND_WORKSHOP, KIND_WATER, KIND_STONE = range(5)
+GOAL_OTHER, GOAL_GET, GOAL_MAKE, GOAL_GO, GOAL_USE = range(5)
+
+STEP_AUTORESET = 1
+
+
+class craft_recipe_t(ctypes.Structure):
+    _fields_ = [
+        ("output", ctypes.c_int32),
+        ("workshop", ctypes.c_int32),
+        ("yield_", ctypes.c_int32),
+        ("n_inputs", ctypes.c_int32),
+        ("input_kind", ctypes.c_int32 * MAX_INGREDIENTS),
+        ("input_count", ctypes.c_int32 * MAX_INGREDIENTS),
+    ]
+
+
+class craft_task_t(ctypes.Structure):
+    _fields_ = [
+        ("goal", ctypes.c_int32),
+        ("arg_kind", ctypes.c_int32),
+        ("n_subtasks", ctypes.c_int32),
+        ("subtask", ctypes.c_int32 * MAX_SUBTASKS),
+    ]
+
+
+class craft_config_t(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("window_width", ctypes.c_int32),
+        ("window_height", ctypes.c_int32),
+        ("n_kinds", ctypes.c_int32),
+        ("n_features", ctypes.c_int32),
+        ("max_timesteps", ctypes.c_int32),
+        ("bridge_kind", ctypes.c_int32),
+        ("axe_kind", ctypes.c_int32),
+        ("kind_class", ctypes.c_uint8 * MAX_KINDS),
+        ("n_recipes", ctypes.c_int32),
+        ("recipe", craft_recipe_t * MAX_RECIPES),
+        ("n_tasks", ctypes.c_int32),
+        ("task", craft_task_t * MAX_TASKS),
+    ]
+
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes); exactly the functions include/craft.h declares
+SIGNATURES = {
+    "craft_sim_create": (_i32, [ctypes.POINTER(craft_config_t), _i32, _i64, _i64, _i32,
+                                ctypes.POINTER(_vp)]),
+    "craft_sim_destroy": (_i32, [_vp]),
+    "craft_sim_last_error": (ctypes.c_char_p, [_vp]),
+    "craft_strerror": (ctypes.c_char_p, [_i32]),
+    "craft_sim_info": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32),
+                              ctypes.POINTER(_i32)]),
+    "craft_sim_check": (_i32, [_vp, ctypes.POINTER(_i64), _vp]),
+    "craft_pool_load": (_i32, [_vp, _vp, _i32, _i32]),
+    "craft_reset": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "craft_step": (_i32, [_vp, _vp, _u64, _i64, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "craft_stats": (_i32, [_vp, _vp, _i32, _vp]),
+    "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    "craft_observe": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "craft_teacher": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "craft_get_state": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "craft_set_state": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "craft_sample_scenarios": (_i32, [_i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _u32,
+                                      _i32, _i32, _vp, _vp, _vp]),
+}
+
+
+class CraftError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__(message)
+        self.status = status
+
+
+_lib = None
+
+
+def lib():
+    """The loaded library; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def strerror(status):
+    return lib().craft_strerror(status).decode()
+
+
+def check(status, handle=None, what=""):
+    if status != OK:
+        msg = strerror(status)
+        if handle:
+            detail = lib().craft_sim_last_error(handle)
+            if detail:
+                msg = detail.decode()
+        raise CraftError(status, f"{what}: {msg}" if what else msg)

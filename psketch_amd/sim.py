@@ -1,0 +1,266 @@
+"""Batched CraftWorld simulator on one MI355X: the Python face of the C ABI.
+
+`CraftSim` owns N environment slots in HBM (struct-of-arrays, see
+csrc/craft_sim.hip) and exposes the reference's CraftWorld/CraftState surface
+batched over torch device tensors:
+
+  reset(...)         CraftScenario.init           craft.py:262-273
+  step(actions)      do_rollout tick + features    trainers/imitation.py:59-73, craft.py:296-424
+  transition(a)      CraftState.step               craft.py:332-424
+  observe()          CraftState.features/satisfies craft.py:285-330
+  teacher()          DemonstrationTeacher.__call__ teachers/demonstration.py:9-30
+
+All work runs in HIP kernels on the caller's current torch stream; outputs are
+device tensors the trainer consumes in place (no host round trip).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .cookbook import Cookbook, TaskManager, compile_config, world_params, generator_primitives
+from . import gamedef
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class CraftSim:
+    """N CraftWorld environments on one GPU.
+
+    world: a gamedef.WORLDS name ("craft_medium_12x12" is the benchmark world),
+    a configs/worlds YAML path or a dict.  recipes / hints: YAML paths or None
+    for the built-in tables.  env_id_base: global id of slot 0 (rank * N when
+    sharded), which keys every per-env random draw.
+    """
+
+    def __init__(self, world="craft_medium_12x12", n_envs=4096, device=None, env_id_base=0,
+                 pool_capacity=1024, recipes=None, hints=None,
+                 max_timesteps=gamedef.MAX_TIMESTEPS):
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.params = world_params(world)
+        self.cookbook = Cookbook(recipes)
+        self.task_manager = TaskManager(hints)
+        self.config = compile_config(self.params, self.cookbook, self.task_manager, max_timesteps)
+        self.width, self.height = self.params["WIDTH"], self.params["HEIGHT"]
+        self.n_kinds = self.cookbook.n_kinds
+        self.n_features = self.config.n_features
+        self.n_envs = int(n_envs)
+        self.env_id_base = int(env_id_base)
+        self.pool_capacity = int(pool_capacity)
+        self.pool_count = 0
+        handle = ctypes.c_void_p()
+        N.check(N.lib().craft_sim_create(ctypes.byref(self.config), self.device.index, self.n_envs,
+                                         self.env_id_base, self.pool_capacity,
+                                         ctypes.byref(handle)), what="craft_sim_create")
+        self._h = handle
+
+    # ---- lifetime ---------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().craft_sim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, status, what):
+        N.check(status, self._h, what)
+
+    def check(self):
+        """Synchronises and raises if a kernel latched an error (bad action,
+        teacher assertion, out-of-range slot)."""
+        slot = ctypes.c_int64(-1)
+        self._check(N.lib().craft_sim_check(self._h, ctypes.byref(slot), self._stream()),
+                    "kernel error")
+
+    # ---- helpers --------------------------------------------------------------------
+    def _i32(self, x, n=None):
+        if x is None:
+            return None
+        t = torch.as_tensor(x, device=self.device)
+        if t.dtype != torch.int32:
+            t = t.to(torch.int32)
+        t = t.contiguous()
+        if n is not None and t.numel() != n:
+            raise ValueError(f"expected {n} entries, got {t.numel()}")
+        return t
+
+    def empty_obs(self, n=None):
+        n = self.n_envs if n is None else n
+        return torch.empty((n, self.n_features), dtype=torch.float32, device=self.device)
+
+    # ---- scenario pool -----------------------------------------------------------------
+    def load_pool(self, grids, first=0):
+        """grids: uint8 [P, W, H] or [P, W*H] kind ids (x-major), host or device."""
+        g = np.ascontiguousarray(np.asarray(torch.as_tensor(grids).cpu(), dtype=np.uint8))
+        g = g.reshape(g.shape[0], self.width * self.height)
+        self._check(N.lib().craft_pool_load(self._h, g.ctypes.data_as(ctypes.c_void_p), int(first),
+                                            int(g.shape[0])), "craft_pool_load")
+        self.pool_count = max(self.pool_count, first + g.shape[0])
+
+    def sample_pool(self, count, seed=123, dedup=True):
+        """Generates `count` scenarios with the make_data.py generator
+        (RandomState(seed) stream) and loads them; returns (grids, init_pos)."""
+        grids, init_pos, _ = sample_scenarios(self.params, self.cookbook, seed, count, dedup)
+        self.load_pool(grids)
+        return grids, init_pos
+
+    # ---- episodes -----------------------------------------------------------------------
+    def reset(self, scenario, pos_x, pos_y, dir, task, obs=None):
+        n = self.n_envs
+        args = [self._i32(a, n) for a in (scenario, pos_x, pos_y, dir, task)]
+        self._args_keepalive = args
+        self._check(N.lib().craft_reset(self._h, *[_ptr(a) for a in args], _ptr(obs), self._stream()),
+                    "craft_reset")
+        return obs
+
+    def step(self, actions=None, seed=0, tick=0, autoreset=True, obs=None, reward=None, done=None,
+             success=None):
+        """One rollout tick for every slot (see include/craft.h craft_step).
+        actions: int32 device tensor [N] or None for the in-kernel hashed draw."""
+        a = self._i32(actions, self.n_envs) if actions is not None else None
+        flags = N.STEP_AUTORESET if autoreset else 0
+        self._check(N.lib().craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
+                                       int(tick), flags, _ptr(obs), _ptr(reward), _ptr(done),
+                                       _ptr(success), self._stream()), "craft_step")
+        return obs
+
+    def stats(self, reset=False, out=None):
+        """Device int64[3] {successes, episodes ended, env-steps}."""
+        if out is None:
+            out = torch.zeros(3, dtype=torch.int64, device=self.device)
+        self._check(N.lib().craft_stats(self._h, _ptr(out), int(bool(reset)), self._stream()),
+                    "craft_stats")
+        return out
+
+    # ---- reference-granular surface ----------------------------------------------------
+    def transition(self, actions, src=None, dst=None):
+        a = self._i32(actions)
+        n = a.numel()
+        s, d = self._i32(src, n), self._i32(dst, n)
+        self._check(N.lib().craft_transition(self._h, _ptr(s), _ptr(d), _ptr(a), n, self._stream()),
+                    "craft_transition")
+
+    def observe(self, slots=None, tasks=None, obs=None, sat=None, n=None):
+        s = self._i32(slots)
+        n = s.numel() if s is not None else (self.n_envs if n is None else n)
+        t = self._i32(tasks, n)
+        self._check(N.lib().craft_observe(self._h, _ptr(s), n, _ptr(t), _ptr(obs), _ptr(sat),
+                                          self._stream()), "craft_observe")
+        return obs, sat
+
+    def teacher(self, slots=None, tasks=None, action_out=None, path_len_out=None, n=None):
+        s = self._i32(slots)
+        n = s.numel() if s is not None else (self.n_envs if n is None else n)
+        t = self._i32(tasks, n)
+        if action_out is None:
+            action_out = torch.empty(n, dtype=torch.int32, device=self.device)
+        self._check(N.lib().craft_teacher(self._h, _ptr(s), n, _ptr(t), _ptr(action_out),
+                                          _ptr(path_len_out), self._stream()), "craft_teacher")
+        return action_out, path_len_out
+
+    def get_state(self, slots=None, n=None):
+        s = self._i32(slots)
+        n = s.numel() if s is not None else (self.n_envs if n is None else n)
+        dev = self.device
+        agent = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        inv = torch.empty((n, self.n_kinds), dtype=torch.int32, device=dev)
+        grid = torch.empty((n, self.width * self.height), dtype=torch.uint8, device=dev)
+        spec = torch.empty((n, 5), dtype=torch.int32, device=dev)
+        self._check(N.lib().craft_get_state(self._h, _ptr(s), n, _ptr(agent), _ptr(inv), _ptr(grid),
+                                            _ptr(spec), self._stream()), "craft_get_state")
+        return dict(agent=agent, inventory=inv, grid=grid, spec=spec)
+
+    def set_state(self, spec, agent, inventory=None, slots=None):
+        sp = self._i32(spec)
+        n = sp.shape[0]
+        ag = self._i32(agent)
+        iv = self._i32(inventory)
+        s = self._i32(slots, n)
+        self._check(N.lib().craft_set_state(self._h, _ptr(s), n, _ptr(sp), _ptr(ag), _ptr(iv),
+                                            self._stream()), "craft_set_state")
+
+
+# ---- host-side inputs ---------------------------------------------------------------------
+
+def sample_scenarios(params, cookbook, seed, count, dedup=True):
+    """make_data.sample_scenario (make_data.py:105-144) x count, native and
+    bit-exact against numpy's RandomState(seed).  Returns (grids uint8
+    [count, W*H], init_pos int32 [count, 2], mt_state uint32[625])."""
+    W, H = params["WIDTH"], params["HEIGHT"]
+    prims = np.asarray(generator_primitives(cookbook), dtype=np.int32)
+    ws = np.asarray([cookbook.index["workshop%d" % i] for i in range(params["N_WORKSHOPS"])],
+                    dtype=np.int32)
+    grids = np.zeros((count, W * H), dtype=np.uint8)
+    init_pos = np.zeros((count, 2), dtype=np.int32)
+    mt = np.zeros(625, dtype=np.uint32)
+    st = N.lib().craft_sample_scenarios(
+        W, H, cookbook.index["boundary"], prims.ctypes.data_as(ctypes.c_void_p), len(prims),
+        params["N_PRIMITIVES"], ws.ctypes.data_as(ctypes.c_void_p), len(ws), seed, count,
+        int(bool(dedup)), grids.ctypes.data_as(ctypes.c_void_p),
+        init_pos.ctypes.data_as(ctypes.c_void_p), mt.ctypes.data_as(ctypes.c_void_p))
+    N.check(st, what="craft_sample_scenarios")
+    return grids, init_pos, mt
+
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def hash_actions(seed, gids, tick):
+    """The in-kernel action draw of craft_step: splitmix64(seed ^ (gid<<20) ^ tick) >> 32 mod 6."""
+    g = np.asarray(gids, dtype=np.uint64)
+    key = np.uint64(seed) ^ (g << np.uint64(20)) ^ np.uint64(tick)
+    return ((splitmix64(key) >> np.uint64(32)) % np.uint64(6)).astype(np.int32)
+
+
+def synthetic_specs(grids, width, height, n_envs, env_id_base=0, seed=0, task_ids=None):
+    """Per-env initial states for synthetic rollouts, keyed by global env id:
+    scenario gid mod P, an interior free cell picked by splitmix64, dir 0
+    (init_state's default, craft.py:258), task task_ids[gid mod len].
+    Returns int32 arrays (scenario, x, y, dir, task)."""
+    grids = np.asarray(grids, dtype=np.uint8).reshape(len(grids), width * height)
+    P = len(grids)
+    gid = np.arange(env_id_base, env_id_base + n_envs, dtype=np.int64)
+    scen = (gid % P).astype(np.int64)
+    cells = np.arange(width * height)
+    cx, cy = cells // height, cells % height
+    interior = (cx > 0) & (cx < width - 1) & (cy > 0) & (cy < height - 1)
+    free = (grids == 0) & interior[None, :]
+    n_free = free.sum(axis=1)
+    if (n_free == 0).any():
+        raise ValueError("a scenario has no free interior cell")
+    # rank of each free cell within its scenario, x-major
+    order = np.cumsum(free, axis=1) - 1
+    key = (np.uint64(seed) << np.uint64(32)) ^ gid.astype(np.uint64) ^ np.uint64(0xA5A5A5A5A5A5A5A5)
+    k = ((splitmix64(key) >> np.uint64(32)) % n_free[scen].astype(np.uint64)).astype(np.int64)
+    # cell index of the k-th free cell of each env's scenario
+    pick = np.argmax((order[scen] == k[:, None]) & free[scen], axis=1)
+    x = (pick // height).astype(np.int32)
+    y = (pick % height).astype(np.int32)
+    if task_ids is None:
+        task_ids = np.arange(1, dtype=np.int32)
+    task_ids = np.asarray(task_ids, dtype=np.int32)
+    task = task_ids[gid % len(task_ids)].astype(np.int32)
+    return scen.astype(np.int32), x, y, np.zeros(n_envs, dtype=np.int32), task

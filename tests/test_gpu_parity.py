@@ -1,0 +1,308 @@
+"""Parity of the HIP path (through the C ABI) against the reference fixtures and
+the CPU oracle.  Bit-exact everywhere: every quantity is integer (features are
+small integers in fp32)."""
+import numpy as np
+import pytest
+import torch
+
+from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
+from psketch_amd import _native as N
+from tests.helpers import make_tables, world_for
+
+pytestmark = pytest.mark.gpu
+
+
+def sim_with_pool(world, n, pool, **kw):
+    sim = CraftSim(world, n_envs=n, device=0, pool_capacity=max(1, len(pool)), **kw)
+    sim.load_pool(pool)
+    return sim
+
+
+def set_states(sim, grids_idx, agent, inv, task=None, dirs=None):
+    """Slots 0..n-1 := (pool entry, x, y, dir, inventory)."""
+    n = len(grids_idx)
+    agent = np.asarray(agent, dtype=np.int32)
+    task = np.zeros(n, dtype=np.int32) if task is None else np.asarray(task, dtype=np.int32)
+    spec = np.stack([np.asarray(grids_idx), agent[:, 0], agent[:, 1], agent[:, 2], task], 1)
+    ag = np.concatenate([agent[:, :3], np.full((n, 1), 40)], 1)
+    K = sim.n_kinds
+    iv = np.zeros((n, K), dtype=np.int32)
+    inv = np.asarray(inv)
+    iv[:, :inv.shape[1]] = inv[:, :K]
+    sim.set_state(spec, ag, iv)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def test_edge_kats(golden):
+    cases = golden("kat_edges.json")
+    pool = np.asarray([c["grid"] for c in cases], dtype=np.uint8)
+    sim = sim_with_pool("craft_medium", len(cases), pool)
+    set_states(sim, np.arange(len(cases)), [c["pos"] + [c["dir"]] for c in cases],
+               [c["inv"] for c in cases])
+    sim.transition(torch.tensor([c["action"] for c in cases], dtype=torch.int32, device="cuda"))
+    st = sim.get_state()
+    sim.check()
+    for i, c in enumerate(cases):
+        assert host(st["agent"][i, :3]).tolist() == c["post_pos"] + [c["post_dir"]], c["name"]
+        assert host(st["inventory"][i]).tolist() == c["post_inv"], c["name"]
+        assert host(st["grid"][i]).tolist() == c["post_grid"], c["name"]
+
+
+@pytest.mark.parametrize("W", [8, 12])
+def test_random_step_kats(golden, W):
+    g = golden("kat_step.npz")
+    p = f"w{W}_"
+    n = len(g[p + "action"])
+    sim = sim_with_pool(world_for(W, 3), n, g[p + "pre_grid"])
+    set_states(sim, np.arange(n), g[p + "pre_agent"], g[p + "pre_inv"])
+    obs = sim.empty_obs(n)
+    sim.observe(obs=obs, n=n)
+    np.testing.assert_array_equal(host(obs), g[p + "features"].astype(np.float32))
+    sat = torch.empty(n, dtype=torch.int8, device="cuda")
+    for t in range(g[p + "satisfies"].shape[1]):
+        sim.observe(tasks=torch.full((n,), t, dtype=torch.int32, device="cuda"), sat=sat, n=n)
+        np.testing.assert_array_equal(host(sat), g[p + "satisfies"][:, t], err_msg=f"task {t}")
+    sim.transition(torch.as_tensor(g[p + "action"].astype(np.int32), device="cuda"))
+    st = sim.get_state()
+    sim.check()
+    np.testing.assert_array_equal(host(st["agent"][:, :3]), g[p + "post_agent"])
+    np.testing.assert_array_equal(host(st["inventory"]), g[p + "post_inv"])
+    np.testing.assert_array_equal(host(st["grid"]), g[p + "post_grid"])
+
+
+def test_copy_on_step_keeps_old_state(golden):
+    g = golden("kat_step.npz")
+    sim = sim_with_pool("craft_medium_12x12", 4, g["w12_pre_grid"][:2])
+    set_states(sim, [0, 1, 0, 1], g["w12_pre_agent"][[0, 1, 0, 1]], g["w12_pre_inv"][[0, 1, 0, 1]])
+    before = {k: host(v) for k, v in sim.get_state().items()}
+    src = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+    dst = torch.tensor([2, 3], dtype=torch.int32, device="cuda")
+    acts = torch.as_tensor(g["w12_action"][:2].astype(np.int32), device="cuda")
+    sim.transition(acts, src, dst)
+    after = {k: host(v) for k, v in sim.get_state().items()}
+    sim.check()
+    for k in before:
+        np.testing.assert_array_equal(after[k][:2], before[k][:2])
+    np.testing.assert_array_equal(after["agent"][2:, :3], g["w12_post_agent"][:2])
+    np.testing.assert_array_equal(after["grid"][2:], g["w12_post_grid"][:2])
+
+
+@pytest.mark.parametrize("split", ["dev", "test"])
+def test_replay_reference_demonstrations_on_gpu(golden, split):
+    """The reference's committed demonstrations, replayed on the GPU: the GPU
+    teacher reproduces every action and every episode ends satisfied."""
+    g = golden("devtest.npz")
+    n = len(g[f"{split}_task"])
+    sim = sim_with_pool("craft_medium", n, g[f"{split}_grids"])
+    pos = g[f"{split}_pos"].astype(np.int32)
+    agent = np.concatenate([pos, np.zeros((n, 1), np.int32)], 1)
+    set_states(sim, g[f"{split}_world"], agent, np.zeros((n, 1)), task=g[f"{split}_task"])
+    acts = g[f"{split}_actions"].astype(np.int32)
+    for t in range(acts.shape[1]):
+        ta, _ = sim.teacher(n=n)
+        ta = host(ta)
+        live = acts[:, t] >= 0
+        np.testing.assert_array_equal(ta[live], acts[live, t], err_msg=f"t={t}")
+        step = np.where(live & (acts[:, t] != N.STOP), acts[:, t], -1).astype(np.int32)
+        sim.transition(torch.as_tensor(step, device="cuda"))
+    sat = torch.empty(n, dtype=torch.int8, device="cuda")
+    sim.observe(sat=sat, n=n)
+    sim.check()
+    assert (host(sat) == 1).all()
+
+
+def test_teacher_12x12(golden):
+    g = golden("teacher_12x12.npz")
+    n = len(g["grid"])
+    sim = sim_with_pool("craft_medium_12x12", n, g["grid"])
+    set_states(sim, np.arange(n), g["agent"], g["inv"])
+    plen = torch.empty(n, dtype=torch.int32, device="cuda")
+    n_tasks = g["action"].shape[1]
+    for t in range(n_tasks):
+        tasks = torch.full((n,), t, dtype=torch.int32, device="cuda")
+        a, _ = sim.teacher(tasks=tasks, path_len_out=plen, n=n)
+        np.testing.assert_array_equal(host(a), g["action"][:, t], err_msg=f"task {t}")
+        ref = g["path_len"][:, t]
+        if (ref != -3).all():
+            np.testing.assert_array_equal(host(plen), ref, err_msg=f"task {t}")
+        try:
+            sim.check()
+        except N.CraftError as e:
+            assert e.status == N.ETEACHER and (g["action"][:, t] == -2).any()
+
+
+@pytest.mark.parametrize("window", [3, 5])
+def test_rollout_fixture(golden, window):
+    g = golden(f"rollout_12x12_w{window}.npz")
+    E = g["spec"].shape[0]
+    sim = sim_with_pool(world_for(12, window), E, g["pool"])
+    sp = g["spec"]
+    sim.reset(sp[:, 0], sp[:, 1], sp[:, 2], sp[:, 3], sp[:, 4])
+    obs = sim.empty_obs()
+    rew = torch.empty(E, dtype=torch.float32, device="cuda")
+    done = torch.empty(E, dtype=torch.uint8, device="cuda")
+    succ = torch.empty(E, dtype=torch.int8, device="cuda")
+    ticks = list(g["obs_ticks"])
+    seed = int(g["seed"][0])
+    for t in range(g["done"].shape[0]):
+        sim.step(seed=seed, tick=t, obs=obs, reward=rew, done=done, success=succ)
+        st = sim.get_state()
+        np.testing.assert_array_equal(host(done), g["done"][t])
+        np.testing.assert_array_equal(host(succ), g["success"][t])
+        np.testing.assert_array_equal(host(rew), g["reward"][t].astype(np.float32))
+        np.testing.assert_array_equal(host(st["agent"]), g["agent"][t])
+        np.testing.assert_array_equal(host(st["inventory"]), g["inv"][t])
+        np.testing.assert_array_equal(host(st["grid"]), g["grid"][t])
+        if t in ticks:
+            np.testing.assert_array_equal(host(obs), g["obs"][ticks.index(t)].astype(np.float32))
+    sim.check()
+
+
+def oracle_from_sim_specs(oracle_mod, cfg, pool, specs):
+    o = oracle_mod.Oracle(cfg, pool)
+    envs = o.init_envs(*specs)
+    return o, envs
+
+
+@pytest.mark.parametrize("window,autoreset,policy", [(3, True, False), (5, True, False),
+                                                     (3, False, True), (5, True, True)])
+def test_lockstep_vs_oracle_4096(oracle_mod, window, autoreset, policy):
+    """Config 2: 4096 12x12 envs, 100 ticks, bit-exact against the CPU oracle
+    every tick (observation, done, success, reward; full state every 10 ticks)."""
+    world = world_for(12, window)
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 256)
+    n = 4096
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=11, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    sim.reset(*specs)
+    o, envs = oracle_from_sim_specs(oracle_mod, cfg, pool, specs)
+    obs = sim.empty_obs()
+    rew = torch.empty(n, dtype=torch.float32, device="cuda")
+    done = torch.empty(n, dtype=torch.uint8, device="cuda")
+    succ = torch.empty(n, dtype=torch.int8, device="cuda")
+    rng = np.random.RandomState(window)
+    stats = np.zeros(3, dtype=np.int64)
+    T = 100 if autoreset else 50
+    for t in range(T):
+        acts = rng.randint(0, 6, size=n).astype(np.int32) if policy else None
+        sim.step(None if acts is None else torch.as_tensor(acts, device="cuda"), seed=5, tick=t,
+                 autoreset=autoreset, obs=obs, reward=rew, done=done, success=succ)
+        rc, oobs, orew, odone, osucc = o.batch_tick(envs, 0, acts, 5, t, autoreset, True, stats)
+        assert rc == 0
+        np.testing.assert_array_equal(host(done), odone, err_msg=f"t={t}")
+        np.testing.assert_array_equal(host(succ), osucc, err_msg=f"t={t}")
+        np.testing.assert_array_equal(host(rew), orew, err_msg=f"t={t}")
+        np.testing.assert_array_equal(host(obs), oobs, err_msg=f"t={t}")
+        if t % 10 == 9:
+            st = sim.get_state()
+            np.testing.assert_array_equal(host(st["agent"]),
+                                          np.stack([envs["x"], envs["y"], envs["dir"], envs["timer"]], 1))
+            np.testing.assert_array_equal(host(st["inventory"]), envs["inv"][:, :cfg.n_kinds])
+            np.testing.assert_array_equal(host(st["grid"]), envs["grid"][:, :144])
+    np.testing.assert_array_equal(host(sim.stats()), stats)
+    sim.check()
+
+
+def test_full_size_properties_and_sharding(oracle_mod):
+    """Config 3 sizes (65536 envs, 12x12, w=3): determinism, shard invariance
+    (two half-size sims with env_id_base == one full sim), episode accounting,
+    observation invariants, and an oracle spot-check of 256 random envs."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 1024)
+    n, T = 65536, 30
+    tasks = [t.id for t in tm.dataset_tasks()]
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=0, task_ids=tasks)
+
+    def run(base, count):
+        sp = synthetic_specs(pool, 12, 12, count, base, seed=0, task_ids=tasks)
+        sim = CraftSim(world, n_envs=count, device=0, env_id_base=base, pool_capacity=1024)
+        sim.load_pool(pool)
+        sim.reset(*sp)
+        obs = sim.empty_obs()
+        done = torch.empty(count, dtype=torch.uint8, device="cuda")
+        total_done = torch.zeros(count, dtype=torch.int64, device="cuda")
+        for t in range(T):
+            sim.step(seed=1, tick=t, obs=obs, done=done)
+            total_done += done
+        st = sim.get_state()
+        sim.check()
+        return sim, obs, total_done, st
+
+    sim, obs, total_done, st = run(0, n)
+    _, obs2, _, _ = run(0, n)
+    assert torch.equal(obs, obs2)
+    _, oa, _, sa = run(0, n // 2)
+    _, ob, _, sb = run(n // 2, n // 2)
+    assert torch.equal(torch.cat([oa, ob]), obs)
+    for k in st:
+        assert torch.equal(torch.cat([sa[k], sb[k]]), st[k]), k
+    s = host(sim.stats())
+    assert s[2] == n * T and s[1] == int(total_done.sum())
+    o = host(obs)
+    L = 9 * 21
+    assert (o[:, -1] == 0).all()
+    assert (o[:, 2 * L + 21:2 * L + 25].sum(1) == 1).all()
+    assert (o[:, :L].reshape(n, 9, 21).sum(2) <= 1).all()
+    # oracle spot-check on random global ids
+    ids = np.random.RandomState(0).choice(n, 256, replace=False)
+    oc = oracle_mod.Oracle(cfg, pool)
+    for gid in ids:
+        env = oc.init_envs(*[a[gid:gid + 1] for a in specs])
+        for t in range(T):
+            rc, oobs, _, _, _ = oc.batch_tick(env, int(gid), None, 1, t, True)
+        np.testing.assert_array_equal(o[gid], oobs[0], err_msg=str(gid))
+
+
+def test_teacher_at_scale_vs_oracle(oracle_mod):
+    """Config 5: the batched GPU teacher on 65536 envs mid-rollout, checked
+    against the literal per-target BFS oracle on 2048 of them."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 512)
+    n = 65536
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=4, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    sim.reset(*specs)
+    for t in range(7):
+        sim.step(seed=9, tick=t)
+    plen = torch.empty(n, dtype=torch.int32, device="cuda")
+    act, _ = sim.teacher(path_len_out=plen)
+    st = {k: host(v) for k, v in sim.get_state().items()}
+    sim.check()
+    act, plen = host(act), host(plen)
+    o = oracle_mod.Oracle(cfg, pool)
+    for i in np.random.RandomState(1).choice(n, 2048, replace=False):
+        x, y, d, _ = st["agent"][i]
+        env = o.env(st["grid"][i], x, y, d, st["inventory"][i])
+        rc, a = o.teacher(env, int(specs[4][i]))
+        assert rc == 0 and a == act[i], i
+        rc, _, ln = o.closest_resource(env, cfg.task[int(specs[4][i])].arg_kind)
+        assert rc == 0 and ln == plen[i], i
+
+
+def test_bad_action_latches_error():
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 8)
+    sim = sim_with_pool(world, 64, pool)
+    sim.reset(*synthetic_specs(pool, 12, 12, 64, 0, seed=0, task_ids=[12]))
+    acts = torch.zeros(64, dtype=torch.int32, device="cuda")
+    acts[17] = 9
+    sim.step(acts, tick=0)
+    with pytest.raises(N.CraftError) as e:
+        sim.check()
+    assert e.value.status == N.EBADACTION
+    sim.check()   # cleared
+
+
+def test_pool_rejects_open_border():
+    sim = CraftSim("craft_medium", n_envs=8, device=0, pool_capacity=2)
+    g = np.zeros((1, 64), dtype=np.uint8)
+    with pytest.raises(N.CraftError) as e:
+        sim.load_pool(g)
+    assert e.value.status == N.EINVARIANT

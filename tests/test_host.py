@@ -1,0 +1,137 @@
+"""CPU tests of the host side: the C ABI library loads and exports what
+include/craft.h declares, the native scenario generator reproduces the
+reference's random stream, and the host input layout is shard-invariant."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from psketch_amd import _native as N
+from psketch_amd.sim import sample_scenarios, synthetic_specs, hash_actions
+from tests.helpers import make_tables
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "craft.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(craft_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = N.lib()
+    names = header_functions()
+    assert len(names) >= 15
+    for name in names:
+        assert hasattr(lib, name), name
+    assert sorted(N.SIGNATURES) == names
+
+
+def test_config_layout_matches_c(oracle_mod):
+    _, _, _, cfg = make_tables()
+    assert oracle_mod.lib().oracle_sizeof_config() == ctypes.sizeof(cfg)
+
+
+def test_strerror():
+    assert N.strerror(N.EBADACTION) == "Unexpected action"
+    assert N.strerror(N.OK) == "ok"
+
+
+def test_create_rejects_bad_config_without_gpu():
+    _, _, _, cfg = make_tables()
+    cfg.n_features += 1           # craft.py:327 feature-length assertion
+    h = ctypes.c_void_p()
+    st = N.lib().craft_sim_create(ctypes.byref(cfg), 0, 16, 0, 4, ctypes.byref(h))
+    assert st == N.EINVAL and not h.value
+
+
+# ---- scenario generator -------------------------------------------------------------------
+@pytest.mark.parametrize("name,world,count", [("w8", "craft_medium", 100),
+                                              ("w12", "craft_medium_12x12", 64)])
+def test_native_generator_matches_reference_stream(golden, name, world, count):
+    """make_data.sample_scenario run by the reference on RandomState(123)."""
+    g = golden("scenarios_seed123.npz")
+    params, cb, _, _ = make_tables(world)
+    grids, init, mt = sample_scenarios(params, cb, 123, count, dedup=True)
+    np.testing.assert_array_equal(grids, g[f"{name}_grids"])
+    np.testing.assert_array_equal(init, g[f"{name}_init"])
+    np.testing.assert_array_equal(mt[:624], g[f"{name}_mt_key"])
+    assert mt[624] == g[f"{name}_mt_pos"][0]
+
+
+def test_native_mt19937_matches_numpy():
+    params, cb, _, _ = make_tables("craft_medium_12x12")
+    for seed in (0, 1, 2**32 - 1):
+        _, _, mt = sample_scenarios(params, cb, seed, 3, dedup=False)
+        rs = np.random.RandomState(seed)
+        # replay: the native stream must equal numpy's after the same draws
+        from oracle.make_data_oracle import sample_worlds
+        from psketch_amd.cookbook import generator_primitives
+        rs2 = np.random.RandomState(seed)
+        for _ in range(3):
+            from oracle.make_data_oracle import sample_scenario
+            ws = [cb.index["workshop%d" % i] for i in range(3)]
+            sample_scenario(12, 12, cb.index["boundary"], generator_primitives(cb), 2, ws, rs2)
+        st = rs2.get_state()
+        np.testing.assert_array_equal(mt[:624], st[1])
+        assert mt[624] == st[2]
+        del rs
+
+
+def test_make_data_oracle_regenerates_reference_dataset(golden, oracle_mod):
+    """make_data.py with seed 123 reproduces the reference's committed dev/test
+    splits: worlds, task order, init positions, instance ids and teacher
+    demonstrations.  Also the native generator equals the oracle's worlds."""
+    from oracle.make_data_oracle import make_dataset, sample_worlds
+    from psketch_amd.cookbook import generator_primitives
+    params, cb, tm, cfg = make_tables("craft_medium")
+    o = oracle_mod.Oracle(cfg)
+    data = make_dataset(params, cb, tm, o, generator_primitives(cb), seed=123)
+    g = golden("devtest.npz")
+    for split in ("dev", "test"):
+        items = data[split]
+        np.testing.assert_array_equal(np.stack([it["grid"].reshape(-1) for it in items]),
+                                      g[f"{split}_grids"])
+        rows = []
+        for wi, it in enumerate(items):
+            for ti in it["task_instances"]:
+                for pos, iid, acts in zip(ti["init_pos"], ti["ids"], ti["ref_actions"]):
+                    rows.append((wi, ti["task"], tuple(int(v) for v in pos), iid, tuple(acts)))
+        assert [r[0] for r in rows] == g[f"{split}_world"].tolist()
+        assert [r[1] for r in rows] == g[f"{split}_task"].tolist()
+        assert [list(r[2]) for r in rows] == g[f"{split}_pos"].tolist()
+        assert [r[3] for r in rows] == g[f"{split}_ids"].tolist()
+        ref_acts = [tuple(int(a) for a in row if a >= 0) for row in g[f"{split}_actions"]]
+        assert [r[4] for r in rows] == ref_acts
+    assert sum(len(ti["init_pos"]) for it in data["train"] for ti in it["task_instances"]) == 17600
+    worlds, _, _ = sample_worlds(params, cb, generator_primitives(cb), 123, 100)
+    native, _, _ = sample_scenarios(params, cb, 123, 100, dedup=True)
+    np.testing.assert_array_equal(native, np.stack([w.reshape(-1) for w in worlds]))
+
+
+# ---- synthetic inputs --------------------------------------------------------------------
+def test_synthetic_specs_properties_and_shard_invariance():
+    params, cb, tm, _ = make_tables("craft_medium_12x12")
+    grids, _, _ = sample_scenarios(params, cb, 123, 32)
+    tasks = [t.id for t in tm.dataset_tasks()]
+    full = synthetic_specs(grids, 12, 12, 1000, 0, seed=3, task_ids=tasks)
+    scen, x, y, d, task = full
+    assert (grids[scen, x * 12 + y] == 0).all()
+    assert ((x > 0) & (x < 11) & (y > 0) & (y < 11)).all()
+    assert (d == 0).all() and set(task.tolist()) == set(tasks)
+    a = synthetic_specs(grids, 12, 12, 400, 0, seed=3, task_ids=tasks)
+    b = synthetic_specs(grids, 12, 12, 600, 400, seed=3, task_ids=tasks)
+    for fa, fb, ff in zip(a, b, full):
+        np.testing.assert_array_equal(np.concatenate([fa, fb]), ff)
+    again = synthetic_specs(grids, 12, 12, 1000, 0, seed=3, task_ids=tasks)
+    for u, v in zip(full, again):
+        np.testing.assert_array_equal(u, v)
+
+
+def test_hash_actions_uniform():
+    a = hash_actions(0, np.arange(60000), 5)
+    counts = np.bincount(a, minlength=6)
+    assert counts.min() > 9500 and counts.max() < 10500

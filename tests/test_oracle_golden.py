@@ -1,0 +1,180 @@
+"""Pins the CPU oracle (and the host-side table compiler) against the
+reference: its own committed demonstrations and the fixtures that
+tests/golden/make_golden.py produced by running the reference's code."""
+import numpy as np
+import pytest
+
+from psketch_amd import _native as N
+from tests.helpers import make_tables, world_for
+
+
+# ---- static tables ----------------------------------------------------------------------
+def test_cookbook_matches_reference(golden):
+    ref = golden("cookbook.json")
+    params, cb, tm, cfg = make_tables()
+    assert list(cb.index) == ref["index"]
+    assert cb.n_kinds == ref["n_kinds"] == cfg.n_kinds
+    assert list(cb.primitives) == ref["primitives_iter"]
+    assert [[k, {str(a): b for a, b in d.items()}] for k, d in cb.recipes.items()] == ref["recipes"]
+    for k in range(cb.n_kinds):
+        cls = cfg.kind_class[k]
+        if k == 0:
+            continue
+        if k in ref["grabbable_indices"]:
+            assert cls == N.KIND_GRABBABLE
+        elif k in ref["workshop_indices"]:
+            assert cls == N.KIND_WORKSHOP
+        elif k == ref["water_index"]:
+            assert cls == N.KIND_WATER
+        elif k == ref["stone_index"]:
+            assert cls == N.KIND_STONE
+        else:
+            assert cls == N.KIND_INERT
+    for name, F in ref["n_features"].items():
+        assert make_tables(name)[3].n_features == F
+    assert [[t.goal_name, t.goal_arg, [f"{s.goal_name}[{s.goal_arg}]" for s in (t.subtasks or [])]]
+            for t in tm.tasks] == ref["tasks"]
+    goals = {"get": N.GOAL_GET, "make": N.GOAL_MAKE, "go": N.GOAL_GO, "use": N.GOAL_USE}
+    for i, t in enumerate(tm.tasks):
+        assert cfg.task[i].goal == goals.get(t.goal_name, N.GOAL_OTHER)
+        assert cfg.task[i].arg_kind == (cb.index[t.goal_arg] or 0)
+        assert [cfg.task[i].subtask[j] for j in range(cfg.task[i].n_subtasks)] == \
+            [s.id for s in (t.subtasks or [])]
+    for name, (idx, (dx, dy)) in ref["actions"].items():
+        assert idx == getattr(N, name)
+
+
+def test_cookbook_from_reference_yaml_matches_builtin():
+    import os
+    path = "/root/reference/resources/craft/recipes.yaml"
+    hints = "/root/reference/resources/craft/hints.hierarchy.yaml"
+    if not os.path.exists(path):
+        pytest.skip("reference tree not present")
+    from psketch_amd.cookbook import Cookbook, TaskManager
+    a, b = Cookbook(path), Cookbook()
+    assert a.index.contents == b.index.contents and a.recipes == b.recipes
+    assert [repr(t) for t in TaskManager(hints).tasks] == [repr(t) for t in TaskManager().tasks]
+
+
+# ---- step / features / satisfies ---------------------------------------------------------
+def test_oracle_edge_kats(golden, oracle_mod):
+    _, _, _, cfg = make_tables("craft_medium")
+    o = oracle_mod.Oracle(cfg)
+    for c in golden("kat_edges.json"):
+        env = o.env(c["grid"], c["pos"][0], c["pos"][1], c["dir"], c["inv"])
+        assert o.step(env, c["action"]) == 0, c["name"]
+        assert [int(env["x"][0]), int(env["y"][0])] == c["post_pos"], c["name"]
+        assert int(env["dir"][0]) == c["post_dir"], c["name"]
+        assert env["inv"][0, :cfg.n_kinds].tolist() == c["post_inv"], c["name"]
+        assert env["grid"][0, :64].tolist() == c["post_grid"], c["name"]
+
+
+@pytest.mark.parametrize("W", [8, 12])
+def test_oracle_random_step_kats(golden, oracle_mod, W):
+    g = golden("kat_step.npz")
+    p = f"w{W}_"
+    _, _, tm, cfg = make_tables(world_for(W, 3))
+    o = oracle_mod.Oracle(cfg)
+    n = len(g[p + "action"])
+    for i in range(n):
+        x, y, d = g[p + "pre_agent"][i]
+        env = o.env(g[p + "pre_grid"][i], x, y, d, g[p + "pre_inv"][i])
+        np.testing.assert_array_equal(o.features(env), g[p + "features"][i], err_msg=str(i))
+        sats = [o.satisfies(env, t) for t in range(len(tm))]
+        assert sats == g[p + "satisfies"][i].tolist(), i
+        assert o.step(env, int(g[p + "action"][i])) == 0
+        assert [int(env["x"][0]), int(env["y"][0]), int(env["dir"][0])] == g[p + "post_agent"][i].tolist(), i
+        assert env["inv"][0, :cfg.n_kinds].tolist() == g[p + "post_inv"][i].tolist(), i
+        assert env["grid"][0, :W * W].tolist() == g[p + "post_grid"][i].tolist(), i
+
+
+def test_oracle_bad_action(oracle_mod):
+    _, _, _, cfg = make_tables("craft_medium")
+    o = oracle_mod.Oracle(cfg)
+    grid = np.zeros((8, 8), dtype=np.uint8)
+    grid[0, :] = grid[-1, :] = grid[:, 0] = grid[:, -1] = 1
+    env = o.env(grid, 3, 3)
+    assert o.step(env, 6) == N.EBADACTION
+    assert o.step(env, -1) == N.EBADACTION
+
+
+# ---- teacher ----------------------------------------------------------------------------------
+@pytest.mark.parametrize("split", ["dev", "test"])
+def test_oracle_replays_reference_demonstrations(golden, oracle_mod, split):
+    """The reference's own data/craft_medium_{split}.json: every teacher action
+    along every demonstration, and satisfies() at its end (make_data.py:146-152)."""
+    g = golden("devtest.npz")
+    _, _, tm, cfg = make_tables("craft_medium")
+    o = oracle_mod.Oracle(cfg)
+    grids = g[f"{split}_grids"]
+    n_steps = 0
+    for i in range(len(g[f"{split}_task"])):
+        w, t = int(g[f"{split}_world"][i]), int(g[f"{split}_task"][i])
+        x, y = g[f"{split}_pos"][i]
+        env = o.env(grids[w], x, y, 0)
+        for a in g[f"{split}_actions"][i]:
+            if a < 0:
+                break
+            rc, ta = o.teacher(env, t)
+            assert rc == 0 and ta == a, (split, i)
+            if a != N.STOP:
+                assert o.step(env, int(a)) == 0
+                n_steps += 1
+        assert o.satisfies(env, t) == 1
+    assert n_steps > 15000
+
+
+def test_oracle_teacher_12x12(golden, oracle_mod):
+    g = golden("teacher_12x12.npz")
+    _, cb, tm, cfg = make_tables("craft_medium_12x12")
+    o = oracle_mod.Oracle(cfg)
+    for i in range(len(g["grid"])):
+        x, y, d = g["agent"][i]
+        env = o.env(g["grid"][i], x, y, d, g["inv"][i])
+        for t in range(len(tm)):
+            rc, a = o.teacher(env, t)
+            ref = int(g["action"][i, t])
+            if ref == -2:
+                assert rc == N.ETEACHER, (i, t)
+            else:
+                assert rc == 0 and a == ref, (i, t, a, ref)
+            ref_len = int(g["path_len"][i, t])
+            if ref_len != -3:
+                rc, fa, ln = o.closest_resource(env, cfg.task[t].arg_kind)
+                if ref_len == -2:
+                    assert rc == N.ETEACHER
+                else:
+                    assert rc == 0 and ln == ref_len, (i, t, ln, ref_len)
+
+
+# ---- rollout protocol ----------------------------------------------------------------------
+@pytest.mark.parametrize("window", [3, 5])
+def test_oracle_rollout_fixture(golden, oracle_mod, window):
+    g = golden(f"rollout_12x12_w{window}.npz")
+    _, _, tm, cfg = make_tables(world_for(12, window))
+    o = oracle_mod.Oracle(cfg, g["pool"])
+    sp = g["spec"]
+    envs = o.init_envs(sp[:, 0], sp[:, 1], sp[:, 2], sp[:, 3], sp[:, 4])
+    seed = int(g["seed"][0])
+    T = g["done"].shape[0]
+    obs_ticks = list(g["obs_ticks"])
+    for t in range(T):
+        rc, obs, reward, done, success = o.batch_tick(envs, 0, None, seed, t, True)
+        assert rc == 0
+        np.testing.assert_array_equal(done, g["done"][t])
+        np.testing.assert_array_equal(success, g["success"][t])
+        np.testing.assert_array_equal(reward, g["reward"][t])
+        np.testing.assert_array_equal(np.stack([envs["x"], envs["y"], envs["dir"], envs["timer"]], 1),
+                                      g["agent"][t])
+        np.testing.assert_array_equal(envs["inv"][:, :cfg.n_kinds], g["inv"][t])
+        np.testing.assert_array_equal(envs["grid"][:, :144], g["grid"][t])
+        if t in obs_ticks:
+            np.testing.assert_array_equal(obs, g["obs"][obs_ticks.index(t)])
+
+
+def test_hash_action_matches(oracle_mod):
+    from psketch_amd.sim import hash_actions
+    gids = np.arange(0, 5000, 7)
+    for tick in (0, 1, 99, 12345):
+        ref = [oracle_mod.hash_action(42, int(g), tick) for g in gids]
+        assert hash_actions(42, gids, tick).tolist() == ref
