@@ -1,0 +1,208 @@
+// craft_device.h — device-side data layout and helpers shared by the kernels.
+//
+// Per-environment state in HBM (struct-of-arrays, slot = env index on this GPU):
+//   state u64[N]      x:8 | y:8 | dir:2 | frozen:1 | . | timer:8 | scenario:24 | task:8
+//                     (one 8-byte load gives everything a tick needs to start)
+//   init  u32[N]      x0 | y0<<8 | dir0<<16   (read only when an episode restarts)
+//   inv   uint4[N][2] 32 inventory counts, u8  (CraftState.inventory)
+//   mask  uint4[N][2] 256-bit set of cells cleared since the episode started
+//   pool  u8[P][CS]   initial grids as kind ids, x-major, CS = roundup(W*H, 16)
+// A slot's grid is pool[scenario] minus its mask: the reference only ever clears
+// cells (grab, bridge, axe: craft.py:383-410), so an episode restart is a mask
+// clear and no per-env grid copy exists.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "../../include/craft.h"
+
+namespace craft {
+
+constexpr int kTileEnvs = 64;     // envs per workgroup tile
+constexpr int kThreads = 256;     // threads per tile workgroup
+constexpr int kRecipeBytes = 12;  // compact recipe: out, ws, n_in, (kind, count) x 4, pad
+
+enum Mode { MODE_TICK = 0, MODE_TRANSITION = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
+
+struct SimView {
+  const uint8_t* pool;
+  uint64_t* state;
+  uint32_t* init;
+  uint4* inv;
+  uint4* mask;
+  const uint16_t* lut;        // [F]: feature f -> descriptor word | shift<<7 | wide<<12
+  const uint16_t* task_tab;   // [n_tasks]: goal | arg_kind<<4 | n_subtasks<<12
+  const int32_t* task_sub;    // [n_tasks][4] subtask ids
+  int64_t* stats_part;        // [n_tiles][4]
+  int32_t* err;               // [4] {code, pad, slot lo, slot hi}
+  int64_t n_envs, env_base;
+  int32_t pool_count, n_tasks, n_recipes;
+  int32_t W, H, K, F, C, CS, GS, maxT;
+  int32_t ND;                 // descriptor row stride in words (odd)
+  int32_t bridge, axe;
+  int32_t lds_desc, lds_lut, lds_task, lds_rc, lds_agent;     // dynamic-LDS byte offsets
+  uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
+  uint32_t magicQ;            // floor(2^32 / (F/4)) + 1
+  const uint8_t* rc;          // [CRAFT_MAX_RECIPES][kRecipeBytes] compact recipes
+  uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
+};
+
+// Observation descriptor of one env (LDS row, ND words):
+//   [0, w2)          local window cells as one-hot words (1 << kind, kind 0 dropped)
+//   [w2, 2w2)        block-max-pooled big-window kind masks
+//   2w2              1 << dir
+//   2w2 + 1          0 (the trailing constant feature)
+//   2w2 + 2 .. +9    inventory counts, 4 per word (the bytes transition() edits)
+// features() row f = (desc[lut.word] >> lut.shift) & (lut.wide ? 0xff : 1).
+__host__ __device__ constexpr int desc_dir_word(int win) { return 2 * win * win; }
+__host__ __device__ constexpr int desc_inv_word(int win) { return 2 * win * win + 2; }
+__host__ __device__ constexpr int desc_words(int win) { return 2 * win * win + 10; }
+
+struct TileArgs {
+  const int32_t* src;
+  const int32_t* dst;
+  const int32_t* actions;
+  const int32_t* tasks;
+  const int32_t* r_scen;   // MODE_RESET inputs
+  const int32_t* r_x;
+  const int32_t* r_y;
+  const int32_t* r_dir;
+  const int32_t* r_task;
+  uint64_t seed;
+  int64_t tick;
+  int64_t n;
+  uint32_t flags;
+  float* obs;
+  float* reward;
+  uint8_t* done;
+  int8_t* sat;
+};
+
+struct Agent {
+  int x, y, dir, frozen, timer, scen, task;
+};
+
+__device__ __forceinline__ Agent unpack_state(uint64_t s) {
+  Agent a;
+  const uint32_t lo = (uint32_t)s, hi = (uint32_t)(s >> 32);
+  a.x = lo & 0xff;
+  a.y = (lo >> 8) & 0xff;
+  a.dir = (lo >> 16) & 3;
+  a.frozen = (lo >> 18) & 1;
+  a.timer = lo >> 24;
+  a.scen = hi & 0xffffff;
+  a.task = hi >> 24;
+  return a;
+}
+
+__device__ __forceinline__ uint64_t pack_state(const Agent& a) {
+  const uint32_t lo = (uint32_t)a.x | ((uint32_t)a.y << 8) | ((uint32_t)a.dir << 16) |
+                      ((uint32_t)a.frozen << 18) | ((uint32_t)a.timer << 24);
+  const uint32_t hi = ((uint32_t)a.scen & 0xffffff) | ((uint32_t)a.task << 24);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+__device__ __forceinline__ void latch_error(int32_t* err, int code, int64_t slot) {
+  if (atomicCAS(err, 0, code) == 0) {
+    err[2] = (int32_t)(slot & 0xffffffff);
+    err[3] = (int32_t)(slot >> 32);
+  }
+}
+
+__device__ __forceinline__ int kind_class(const SimView& v, int k) {
+  return (int)(((k < 16) ? (v.kc_lo >> (4 * k)) : (v.kc_hi >> (4 * (k - 16)))) & 0xf);
+}
+
+__device__ __forceinline__ int dir_dx(int d) { return d == CRAFT_LEFT ? -1 : (d == CRAFT_RIGHT ? 1 : 0); }
+__device__ __forceinline__ int dir_dy(int d) { return d == CRAFT_DOWN ? -1 : (d == CRAFT_UP ? 1 : 0); }
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Sets bit c of a register-resident 8-word mask (static indices only).
+__device__ __forceinline__ void mask_set(uint32_t (&m)[8], int c) {
+  const int w = c >> 5;
+  const uint32_t b = 1u << (c & 31);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] |= (i == w) ? b : 0u;
+}
+
+// CraftState.step (craft.py:332-424) on an LDS grid row `g` and inventory
+// bytes `iv`; `rc_tab` is the compact recipe table (LDS).  Records whether inventory / mask changed.
+__device__ __forceinline__ void transition(const SimView& v, const uint8_t* rc_tab, uint8_t* g, uint8_t* iv, Agent& s,
+                                           uint32_t (&m)[8], int a, bool& inv_changed,
+                                           bool& mask_changed) {
+  const int H = v.H;
+  int dx = 0, dy = 0, ndir = s.dir;
+  if (a < CRAFT_USE) {                               // moves always turn (craft.py:341-352)
+    dx = dir_dx(a);
+    dy = dir_dy(a);
+    ndir = a;
+  } else if (a == CRAFT_USE) {                       // craft.py:356-412
+    const int d = s.dir;
+    const bool ok = (d == CRAFT_LEFT && s.x > 0) || (d == CRAFT_DOWN && s.y > 0) ||
+                    (d == CRAFT_RIGHT && s.x < v.W - 1) || (d == CRAFT_UP && s.y < H - 1);
+    if (ok) {
+      const int c = (s.x + dir_dx(d)) * H + (s.y + dir_dy(d));
+      const int thing = g[c];
+      if (thing != 0) {
+        const int cls = kind_class(v, thing);
+        if (cls == CRAFT_KIND_GRABBABLE) {           // craft.py:383-386
+          iv[thing] = (uint8_t)(iv[thing] + 1);
+          g[c] = 0;
+          mask_set(m, c);
+          inv_changed = mask_changed = true;
+        } else if (cls == CRAFT_KIND_WORKSHOP) {     // recipes in dict order, craft.py:388-401
+          for (int r = 0; r < v.n_recipes; ++r) {
+            const uint8_t* rc = rc_tab + kRecipeBytes * r;
+            if (rc[1] != thing) continue;
+            const int n_in = rc[2];
+            bool have = true;
+            for (int i = 0; i < n_in; ++i) have = have && iv[rc[3 + 2 * i]] >= rc[4 + 2 * i];
+            if (!have) continue;
+            iv[rc[0]] = (uint8_t)(iv[rc[0]] + 1);    // `_yield` 1 (validated at create)
+            for (int i = 0; i < n_in; ++i) iv[rc[3 + 2 * i]] = (uint8_t)(iv[rc[3 + 2 * i]] - rc[4 + 2 * i]);
+            inv_changed = true;
+          }
+        } else if (cls == CRAFT_KIND_WATER) {        // craft.py:403-406
+          if (iv[v.bridge] > 0) {
+            g[c] = 0;
+            mask_set(m, c);
+            iv[v.bridge] = (uint8_t)(iv[v.bridge] - 1);
+            inv_changed = mask_changed = true;
+          }
+        } else if (cls == CRAFT_KIND_STONE) {        // craft.py:408-410 (axe kept)
+          if (iv[v.axe] > 0) {
+            g[c] = 0;
+            mask_set(m, c);
+            mask_changed = true;
+          }
+        }
+      }
+    }
+  }
+  // Collision against the pre-action grid (craft.py:418-421); USE/STOP do not move.
+  if (dx | dy) {
+    const int nx = s.x + dx, ny = s.y + dy;
+    if (g[nx * H + ny] == 0) { s.x = nx; s.y = ny; }
+  }
+  s.dir = ndir;
+}
+
+// CraftState.satisfies (craft.py:285-294): 1/0, -1 for None.  `tt` is the
+// task-table entry goal | arg<<4.
+__device__ __forceinline__ int satisfies(const SimView& v, const uint8_t* g, const uint8_t* iv,
+                                         const Agent& s, uint32_t tt) {
+  const int goal = tt & 0xf, arg = (tt >> 4) & 0xff;
+  if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) return iv[arg] > 0;
+  if (goal == CRAFT_GOAL_GO) return g[(s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir))] == arg;
+  return -1;
+}
+
+}  // namespace craft

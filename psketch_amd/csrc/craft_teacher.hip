@@ -1,0 +1,327 @@
+// craft_teacher.hip — DemonstrationTeacher on the GPU: the hint-tree walk of
+// BaseTeacher.find_incomplete_subtask and find_closest_resources' BFS, one lane
+// per env, the BFS held as per-direction position bitsets in registers.
+#include "craft_device.h"
+
+namespace craft {
+
+template <int NW>
+struct Bits {
+  uint64_t w[NW];
+};
+
+template <int NW>
+__device__ __forceinline__ Bits<NW> bzero() {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = 0;
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> band(const Bits<NW>& a, const Bits<NW>& b) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] & b.w[i];
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> bor(const Bits<NW>& a, const Bits<NW>& b) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] | b.w[i];
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> bandn(const Bits<NW>& a, const Bits<NW>& b) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] & ~b.w[i];
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ bool bany(const Bits<NW>& a) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) x |= a.w[i];
+  return x != 0;
+}
+template <int NW>
+__device__ __forceinline__ bool btest(const Bits<NW>& a, int p) {
+  uint64_t x = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) x |= (i == (p >> 6)) ? a.w[i] : 0ull;
+  return (x >> (p & 63)) & 1ull;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> bbit(int p) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = (i == (p >> 6)) ? (1ull << (p & 63)) : 0ull;
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ int blowest(const Bits<NW>& a) {   // INT_MAX if empty
+  int r = INT_MAX;
+#pragma unroll
+  for (int i = NW - 1; i >= 0; --i)
+    if (a.w[i]) r = i * 64 + __ffsll((unsigned long long)a.w[i]) - 1;
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ int bhighest(const Bits<NW>& a) {  // -1 if empty
+  int r = -1;
+#pragma unroll
+  for (int i = 0; i < NW; ++i)
+    if (a.w[i]) r = i * 64 + 63 - __clzll((long long)a.w[i]);
+  return r;
+}
+// p -> p + d for every member (|d| < 64); members shifted past either end drop out.
+template <int NW>
+__device__ __forceinline__ Bits<NW> bshift(const Bits<NW>& a, int d) {
+  Bits<NW> r;
+  if (d > 0) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) r.w[i] = (a.w[i] << d) | (i > 0 ? a.w[i - 1] >> (64 - d) : 0ull);
+  } else {
+    const int s = -d;
+#pragma unroll
+    for (int i = 0; i < NW; ++i)
+      r.w[i] = (a.w[i] >> s) | (i + 1 < NW ? a.w[i + 1] << (64 - s) : 0ull);
+  }
+  return r;
+}
+
+// find_closest_resources (teachers/base.py:27-34) over shortest_path
+// (teachers/base.py:36-87) as ONE level-synchronous BFS over (pos, dir) states
+// held as per-direction position bitsets.  FIFO order within a level is
+// sorted by the path's first action (induction: level 1 is enqueued in action
+// order DOWN, UP, LEFT, RIGHT, and children keep their first-dequeued parent's
+// label), so tracking the level's states per first action (a "label")
+// reproduces exactly which state the reference dequeues first:
+//   a target's path length = the first level at which a state faces it,
+//   its first action = the smallest label among that level's facing states,
+//   the chosen target = the first in np.nonzero (x-major) order with the
+//   minimal length (strict `<`, base.py:31).
+// Returns false where the reference raises (len(None) on an unreachable
+// target after a reachable one, base.py:31).
+template <int NW>
+__device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
+                            int H, int p0, int d0, int& first_action, int& path_len) {
+  const int dl[4] = {-1, 1, -H, H};   // DOWN, UP, LEFT, RIGHT in x-major cell index
+  const Bits<NW> fr = bandn(valid, occ);
+  Bits<NW> V[4], cur[4], fc[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) V[a] = bzero<NW>();
+#pragma unroll
+  for (int a = 0; a < 4; ++a) V[a] = (a == d0) ? bbit<NW>(p0) : V[a];
+  Bits<NW> claimed = bzero<NW>();
+  bool found = false;
+  first_action = -1;
+  path_len = -1;
+  {
+    const int f0 = p0 + dl[d0];            // start state already faces a target: []
+    if (f0 >= 0 && btest(tgt, f0)) {
+      found = true;
+      path_len = 0;
+      claimed = bbit<NW>(f0);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int q0 = p0 + dl[a];
+    const int q = btest(fr, q0) ? q0 : p0;
+    if (!btest(V[a], q)) {
+      V[a] = bor(V[a], bbit<NW>(q));
+      cur[a] = bbit<NW>(q);
+      fc[a] = band(bshift(cur[a], dl[a]), valid);
+    } else {
+      cur[a] = bzero<NW>();
+      fc[a] = bzero<NW>();
+    }
+  }
+  Bits<NW> blk[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) blk[a] = bshift(occ, -dl[a]);   // blk[a][p] = occ[p + dl[a]]
+  int depth = 1;
+  while (bany(bor(bor(cur[0], cur[1]), bor(cur[2], cur[3])))) {
+    int bp = INT_MAX, bl = -1;
+#pragma unroll
+    for (int lab = 0; lab < 4; ++lab) {
+      const Bits<NW> hit = bandn(band(fc[lab], tgt), claimed);
+      if (bany(hit)) {
+        claimed = bor(claimed, hit);
+        const int p = blowest(hit);
+        if (p < bp) { bp = p; bl = lab; }
+      }
+    }
+    if (!found && bl >= 0) {
+      found = true;
+      path_len = depth;
+      first_action = bl;
+    }
+    if (!bany(bandn(tgt, claimed))) break;
+    Bits<NW> nc[4], nf[4];
+#pragma unroll
+    for (int lab = 0; lab < 4; ++lab) {
+      nc[lab] = bzero<NW>();
+      nf[lab] = bzero<NW>();
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const Bits<NW> moved = bor(band(bshift(cur[lab], dl[a]), fr), band(cur[lab], blk[a]));
+        const Bits<NW> fresh = bandn(moved, V[a]);
+        V[a] = bor(V[a], fresh);
+        nc[lab] = bor(nc[lab], fresh);
+        nf[lab] = bor(nf[lab], band(bshift(fresh, dl[a]), valid));
+      }
+    }
+#pragma unroll
+    for (int lab = 0; lab < 4; ++lab) { cur[lab] = nc[lab]; fc[lab] = nf[lab]; }
+    ++depth;
+  }
+  if (found) {
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  }
+  return true;
+}
+
+
+struct TeachArgs {
+  const int32_t* slots;
+  const int32_t* tasks;
+  int64_t n;
+  int32_t* act_out;
+  int32_t* len_out;
+};
+
+__device__ __forceinline__ int grid_kind(const SimView& v, int scen, const uint32_t (&m)[8], int c) {
+  const int k = v.pool[(size_t)scen * v.CS + c];
+  uint32_t mw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mw |= (i == (c >> 5)) ? m[i] : 0u;
+  return ((mw >> (c & 31)) & 1u) ? 0 : k;
+}
+
+// DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30), one lane per slot.
+template <int NW>
+__global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const int64_t slot = a.slots ? (int64_t)a.slots[i] : i;
+  if (slot < 0 || slot >= v.n_envs) {
+    latch_error(v.err, CRAFT_ERANGE, i);
+    a.act_out[i] = -2;
+    if (a.len_out) a.len_out[i] = -2;
+    return;
+  }
+  const Agent s = unpack_state(v.state[slot]);
+  const int task = a.tasks ? a.tasks[i] : s.task;
+  if (task < 0 || task >= v.n_tasks || s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 ||
+      s.scen >= v.pool_count) {
+    latch_error(v.err, task < 0 || task >= v.n_tasks ? CRAFT_ERANGE : CRAFT_EINVAL, i);
+    a.act_out[i] = -2;
+    if (a.len_out) a.len_out[i] = -2;
+    return;
+  }
+  uint32_t m[8];
+  {
+    const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+    m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
+    m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
+  }
+  const uint8_t* iv = reinterpret_cast<const uint8_t*>(v.inv + 2 * slot);
+  const int H = v.H, C = v.C;
+  const int facing = grid_kind(v, s.scen, m, (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir)));
+
+  auto sat = [&](int t) -> int {       // satisfies(), craft.py:285-294
+    const uint32_t tt = v.task_tab[t];
+    const int goal = tt & 0xf, arg = (tt >> 4) & 0xff;
+    if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) return iv[arg] > 0;
+    if (goal == CRAFT_GOAL_GO) return facing == arg;
+    return -1;
+  };
+
+  Bits<NW> valid = bzero<NW>();
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int nb = min(64, max(0, C - w * 64));
+    valid.w[w] = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
+  }
+  auto closest = [&](int kind, int& fa, int& len) -> bool {
+    Bits<NW> occ = bzero<NW>(), tgt = bzero<NW>();
+    for (int c = 0; c < C; ++c) {
+      const int k = grid_kind(v, s.scen, m, c);
+      if (k) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const uint64_t b = (w == (c >> 6)) ? (1ull << (c & 63)) : 0ull;
+          occ.w[w] |= b;
+          if (k == kind) tgt.w[w] |= b;
+        }
+      }
+    }
+    return bfs_closest<NW>(occ, tgt, valid, H, s.x * H + s.y, s.dir, fa, len);
+  };
+
+  int action = CRAFT_STOP;
+  int err = 0;
+  // find_incomplete_subtask, teachers/base.py:10-25
+  int node = task;
+  if (sat(node) != 1) {
+    for (int guard = 0; guard < CRAFT_MAX_TASKS; ++guard) {
+      const int nsub = (v.task_tab[node] >> 12) & 0xf;
+      if (nsub == 0) break;
+      const int32_t* sub = v.task_sub + CRAFT_MAX_SUBTASKS * node;
+      int chosen = sub[nsub - 1];
+      bool last = true;
+      for (int q = 0; q + 1 < nsub; ++q)
+        if (sat(sub[q]) != 1) { chosen = sub[q]; last = false; break; }
+      if (last && sat(chosen) == 1) { err = CRAFT_ETEACHER; break; }   // base.py:24 assert
+      node = chosen;
+    }
+    if (!err) {
+      const uint32_t lt = v.task_tab[node];
+      const int goal = lt & 0xf, arg = (lt >> 4) & 0xff;
+      if (goal == CRAFT_GOAL_USE) {
+        action = CRAFT_USE;
+      } else if (goal == CRAFT_GOAL_GO) {
+        int fa = -1, len = -1;
+        if (!closest(arg, fa, len)) err = CRAFT_ETEACHER;
+        else if (len < 0) action = CRAFT_STOP;                           // demonstration.py:25-26
+        else if (len == 0) err = CRAFT_ETEACHER;                         // [][0]
+        else action = fa;
+      } else {
+        err = CRAFT_ETEACHER;                                            // demonstration.py:18
+      }
+    }
+  }
+  if (err) {
+    latch_error(v.err, err, slot);
+    action = -2;                       // where the reference raises
+  }
+  a.act_out[i] = action;
+  if (a.len_out) {
+    const int arg = (v.task_tab[task] >> 4) & 0xff;
+    int fa = -1, len = -1;
+    if (arg > 0 && !closest(arg, fa, len)) {
+      latch_error(v.err, CRAFT_ETEACHER, slot);
+      len = -2;
+    }
+    a.len_out[i] = len;
+  }
+}
+
+hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
+                          int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
+  TeachArgs a{slots, tasks, n, act_out, len_out};
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  switch (nw) {
+    case 1: hipLaunchKernelGGL(teacher_kernel<1>, dim3(blocks), dim3(256), 0, st, v, a); break;
+    case 2: hipLaunchKernelGGL(teacher_kernel<2>, dim3(blocks), dim3(256), 0, st, v, a); break;
+    case 3: hipLaunchKernelGGL(teacher_kernel<3>, dim3(blocks), dim3(256), 0, st, v, a); break;
+    default: hipLaunchKernelGGL(teacher_kernel<4>, dim3(blocks), dim3(256), 0, st, v, a); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace craft
