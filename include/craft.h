@@ -139,6 +139,11 @@ const char* craft_strerror(int status);
 int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capacity,
                    int32_t* n_features);
 
+/* Performance knob of the tick / observe kernels (results are identical for
+ * every setting): envs per workgroup tile (16, 32 or 64; 0 = default) and the
+ * most tile workgroups that may share a CU (0 = no cap, else 3..32). */
+int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu);
+
 /* Synchronises `stream` and returns the first kernel-side error latched since
  * the last call (then clears it); *env_out receives the offending slot. */
 int craft_sim_check(craft_sim_t* sim, int64_t* env_out, void* stream);

@@ -20,8 +20,8 @@
 
 namespace craft {
 
-constexpr int kTileEnvs = 64;     // envs per workgroup tile
-constexpr int kThreads = 256;     // threads per tile workgroup
+constexpr int kMaxTileEnvs = 64;  // envs per workgroup tile: 16, 32 or 64 (4 threads per env)
+constexpr int kMinTileEnvs = 16;
 constexpr int kRecipeBytes = 12;  // compact recipe: out, ws, n_in, (kind, count) x 4, pad
 
 enum Mode { MODE_TICK = 0, MODE_TRANSITION = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
@@ -42,7 +42,6 @@ struct SimView {
   int32_t W, H, K, F, C, CS, GS, maxT;
   int32_t ND;                 // descriptor row stride in words (odd)
   int32_t bridge, axe;
-  int32_t lds_desc, lds_lut, lds_task, lds_rc, lds_agent;     // dynamic-LDS byte offsets
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   uint32_t magicQ;            // floor(2^32 / (F/4)) + 1
   const uint8_t* rc;          // [CRAFT_MAX_RECIPES][kRecipeBytes] compact recipes
@@ -59,6 +58,24 @@ struct SimView {
 __host__ __device__ constexpr int desc_dir_word(int win) { return 2 * win * win; }
 __host__ __device__ constexpr int desc_inv_word(int win) { return 2 * win * win + 2; }
 __host__ __device__ constexpr int desc_words(int win) { return 2 * win * win + 10; }
+
+// Dynamic-LDS carve of a tile workgroup (16-byte aligned pieces, Guideline 17):
+// grid rows [tile][GS] | descriptors [tile][ND] u32 | feature LUT [F] u16 |
+// task table [64] u16 | recipes [16][12] | agent words [tile] u32.
+struct LdsLayout {
+  int desc, lut, task, rc, agent, bytes;
+};
+__host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int ND, int F) {
+  auto up16 = [](int x) { return (x + 15) & ~15; };
+  LdsLayout l;
+  l.desc = up16(tile * GS);
+  l.lut = up16(l.desc + tile * ND * 4);
+  l.task = up16(l.lut + (F + 4) * 2);
+  l.rc = up16(l.task + CRAFT_MAX_TASKS * 2);
+  l.agent = up16(l.rc + CRAFT_MAX_RECIPES * kRecipeBytes);
+  l.bytes = up16(l.agent + tile * 4);
+  return l;
+}
 
 struct TileArgs {
   const int32_t* src;

@@ -9,7 +9,8 @@
 #include "craft_device.h"
 
 namespace craft {
-hipError_t launch_tile(int mode, int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
+hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
+                       hipStream_t st);
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st);
 
@@ -120,7 +121,8 @@ struct craft_sim {
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   SimView view{};
-  size_t lds_bytes = 0;
+  int tile = craft::kMaxTileEnvs;   // envs per workgroup of the tick / observe kernels
+  int resident_cap = 0;             // 0: no cap on tile workgroups per CU
   std::string last_error;
 };
 
@@ -205,8 +207,22 @@ std::vector<uint16_t> build_lut(const craft_config_t* c) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// LDS bytes per tile workgroup; a residency cap R pads the request to 160 KiB / R
+// so that at most R tile workgroups share a CU and later tiles' prologues overlap
+// earlier tiles' observation stores.
+size_t lds_bytes(const craft_sim* s, int tile) {
+  const SimView& v = s->view;
+  size_t b = (size_t)craft::lds_layout(tile, v.GS, v.ND, v.F).bytes;
+  if (s->resident_cap > 0) {
+    const size_t capped = ((size_t)163840 / s->resident_cap) & ~size_t(15);
+    if (capped > b) b = capped;
+  }
+  return b;
+}
+
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
-  hipError_t e = craft::launch_tile(mode, s->cfg.window_width, s->view, a, s->lds_bytes,
+  const int tile = (mode == craft::MODE_TICK || mode == craft::MODE_OBSERVE) ? s->tile : craft::kMaxTileEnvs;
+  hipError_t e = craft::launch_tile(mode, s->cfg.window_width, tile, s->view, a, lds_bytes(s, tile),
                                     reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, what);
   return CRAFT_OK;
@@ -247,7 +263,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   s->n_envs = n_envs;
   s->env_base = env_id_base;
   s->pool_capacity = pool_capacity;
-  s->n_tiles = (n_envs + craft::kTileEnvs - 1) / craft::kTileEnvs;
+  s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs;   // stats rows
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
@@ -335,20 +351,19 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   }
   v.magicQ = (uint32_t)((1ull << 32) / (uint64_t)(F / 4 > 0 ? F / 4 : 1)) + 1u;
   v.rc = s->d_rc;
-  auto up16 = [](size_t x) { return (x + 15) & ~size_t(15); };
-  size_t off = up16((size_t)craft::kTileEnvs * GS);
-  v.lds_desc = (int32_t)off;
-  off = up16(off + (size_t)craft::kTileEnvs * ND * 4);
-  v.lds_lut = (int32_t)off;
-  off = up16(off + (size_t)(F + 4) * 2);
-  v.lds_task = (int32_t)off;
-  off = up16(off + CRAFT_MAX_TASKS * 2);
-  v.lds_rc = (int32_t)off;
-  off = up16(off + CRAFT_MAX_RECIPES * craft::kRecipeBytes);
-  v.lds_agent = (int32_t)off;
-  off = up16(off + craft::kTileEnvs * 4);
-  s->lds_bytes = off;
   *out = s;
+  return CRAFT_OK;
+}
+
+int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_cu) {
+  if (!s) return CRAFT_EINVAL;
+  if (tile_envs == 0) tile_envs = craft::kMaxTileEnvs;
+  if (tile_envs != 16 && tile_envs != 32 && tile_envs != 64)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune: tile_envs must be 16, 32 or 64");
+  if (max_resident_per_cu != 0 && (max_resident_per_cu < 3 || max_resident_per_cu > 32))
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune: max_resident_per_cu must be 0 or 3..32");
+  s->tile = tile_envs;
+  s->resident_cap = max_resident_per_cu;
   return CRAFT_OK;
 }
 

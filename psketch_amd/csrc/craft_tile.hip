@@ -50,15 +50,18 @@ __device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int
   return ok ? (1u << k) : 0u;
 }
 
-template <int WIN, int MODE>
-__global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
+template <int WIN, int MODE, int TILE>
+__global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
+  constexpr int kTileEnvs = TILE;
+  constexpr int kThreads = 4 * TILE;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const LdsLayout lay = lds_layout(TILE, v.GS, v.ND, v.F);
   uint8_t* s_grid = smem;
-  uint32_t* s_desc = reinterpret_cast<uint32_t*>(smem + v.lds_desc);
-  uint16_t* s_lut = reinterpret_cast<uint16_t*>(smem + v.lds_lut);
-  uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + v.lds_task);
-  uint8_t* s_rc = smem + v.lds_rc;
-  uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + v.lds_agent);
+  uint32_t* s_desc = reinterpret_cast<uint32_t*>(smem + lay.desc);
+  uint16_t* s_lut = reinterpret_cast<uint16_t*>(smem + lay.lut);
+  uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
+  uint8_t* s_rc = smem + lay.rc;
+  uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
 
   constexpr int kDirWord = desc_dir_word(WIN);
   constexpr int kInvWord = desc_inv_word(WIN);
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
 
   // ---- D: descriptors (local one-hots, pooled kind masks), all threads -----------------
   {
-    const int e = tid & (kTileEnvs - 1), part = tid >> 6;
+    const int e = tid & (kTileEnvs - 1), part = tid / kTileEnvs;
     const uint32_t ag = s_agent[e];
     uint32_t* row = s_desc + e * v.ND;
     const uint8_t* g = s_grid + e * v.GS;
@@ -347,29 +350,42 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   STAMP_END();
 }
 
-template <int WIN, int MODE>
+template <int WIN, int MODE, int TILE>
 static hipError_t launch_one(const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
-  const int64_t tiles = (a.n + kTileEnvs - 1) / kTileEnvs;
+  const int64_t tiles = (a.n + TILE - 1) / TILE;
   if (tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL((tile_kernel<WIN, MODE>), dim3((unsigned)tiles), dim3(kThreads), lds, st, v, a);
+  hipLaunchKernelGGL((tile_kernel<WIN, MODE, TILE>), dim3((unsigned)tiles), dim3(4 * TILE), lds, st, v, a);
   return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t launch_mode(int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+template <int MODE, int TILE>
+static hipError_t launch_win(int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
   switch (win) {
-    case 3: return launch_one<3, MODE>(v, a, lds, st);
-    case 5: return launch_one<5, MODE>(v, a, lds, st);
-    default: return launch_one<7, MODE>(v, a, lds, st);
+    case 3: return launch_one<3, MODE, TILE>(v, a, lds, st);
+    case 5: return launch_one<5, MODE, TILE>(v, a, lds, st);
+    default: return launch_one<7, MODE, TILE>(v, a, lds, st);
   }
 }
 
-hipError_t launch_tile(int mode, int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+template <int MODE>
+static hipError_t launch_tiled(int tile, int win, const SimView& v, const TileArgs& a, size_t lds,
+                               hipStream_t st) {
+  switch (tile) {
+    case 16: return launch_win<MODE, 16>(win, v, a, lds, st);
+    case 32: return launch_win<MODE, 32>(win, v, a, lds, st);
+    default: return launch_win<MODE, 64>(win, v, a, lds, st);
+  }
+}
+
+// The rollout tick and the observation take the tuned tile size; the
+// reference-granular transition / reset always run 64-env tiles.
+hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
+                       hipStream_t st) {
   switch (mode) {
-    case MODE_TICK: return launch_mode<MODE_TICK>(win, v, a, lds, st);
-    case MODE_TRANSITION: return launch_mode<MODE_TRANSITION>(win, v, a, lds, st);
-    case MODE_OBSERVE: return launch_mode<MODE_OBSERVE>(win, v, a, lds, st);
-    default: return launch_mode<MODE_RESET>(win, v, a, lds, st);
+    case MODE_TICK: return launch_tiled<MODE_TICK>(tile, win, v, a, lds, st);
+    case MODE_OBSERVE: return launch_tiled<MODE_OBSERVE>(tile, win, v, a, lds, st);
+    case MODE_TRANSITION: return launch_win<MODE_TRANSITION, 64>(win, v, a, lds, st);
+    default: return launch_win<MODE_RESET, 64>(win, v, a, lds, st);
   }
 }
 

@@ -73,6 +73,11 @@ class CraftSim:
         except Exception:
             pass
 
+    def tune(self, tile_envs=0, max_resident_per_cu=0):
+        """Tick/observe kernel geometry (results are identical for every setting)."""
+        self._check(N.lib().craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu)),
+                    "craft_sim_tune")
+
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 

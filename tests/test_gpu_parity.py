@@ -306,3 +306,38 @@ def test_pool_rejects_open_border():
     with pytest.raises(N.CraftError) as e:
         sim.load_pool(g)
     assert e.value.status == N.EINVARIANT
+
+
+@pytest.mark.parametrize("window", [3, 5])
+def test_tuning_does_not_change_results(window):
+    """craft_sim_tune changes only the kernel geometry: every tile size and
+    residency cap gives bit-identical observations, states and statistics."""
+    world = world_for(12, window)
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 128)
+    n = 5000   # not a multiple of any tile: exercises the partial last tile
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
+    ref = None
+    for tile, cap in [(64, 0), (32, 0), (16, 0), (16, 6), (32, 4), (64, 3)]:
+        sim = sim_with_pool(world, n, pool)
+        sim.tune(tile, cap)
+        sim.reset(*specs)
+        obs = sim.empty_obs()
+        outs = []
+        for t in range(12):
+            sim.step(seed=4, tick=t, obs=obs)
+            outs.append(host(obs).copy())
+        o2 = sim.empty_obs()
+        sim.observe(obs=o2, n=n)
+        outs.append(host(o2))
+        st = {k: host(v) for k, v in sim.get_state().items()}
+        stats = host(sim.stats())
+        sim.check()
+        if ref is None:
+            ref = (outs, st, stats)
+        else:
+            for a, b in zip(outs, ref[0]):
+                np.testing.assert_array_equal(a, b, err_msg=f"tile {tile} cap {cap}")
+            for k in st:
+                np.testing.assert_array_equal(st[k], ref[1][k])
+            np.testing.assert_array_equal(stats, ref[2])
