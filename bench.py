@@ -183,7 +183,8 @@ def main():
                        "max_timesteps": sim.config.max_timesteps},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "tile_kernel<3, MODE_TICK>",
+                         "kernel": f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, "
+                                   f"{ {3: 64, 5: 32}.get(sim.params['WINDOW_WIDTH'], 16)}>",
                          "kernel_us": kernel_ms * 1e3, "bytes_per_env_step": bps},
             "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},
         }

@@ -139,10 +139,14 @@ const char* craft_strerror(int status);
 int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capacity,
                    int32_t* n_features);
 
-/* Performance knob of the tick / observe kernels (results are identical for
- * every setting): envs per workgroup tile (16, 32 or 64; 0 = default) and the
- * most tile workgroups that may share a CU (0 = no cap, else 3..32). */
-int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu);
+/* Performance knobs of the tile kernels (results are identical for every
+ * setting): envs per workgroup tile (16, 32 or 64; 0 = default for the
+ * window), the most tile workgroups that may share a CU (0 = no cap, else
+ * 3..32), and the cache policy of the observation stores (0 write-back,
+ * 1 nontemporal = default, 2 write-through).  Note: craft_sim_tune(.., 0, 0, 0)
+ * selects write-back; pass 1 to keep the default policy. */
+int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu,
+                   int32_t obs_store);
 
 /* Synchronises `stream` and returns the first kernel-side error latched since
  * the last call (then clears it); *env_out receives the offending slot. */

@@ -20,8 +20,10 @@
 
 namespace craft {
 
-constexpr int kMaxTileEnvs = 64;  // envs per workgroup tile: 16, 32 or 64 (4 threads per env)
+constexpr int kThreads = 256;      // threads per tile workgroup
+constexpr int kMaxTileEnvs = 64;   // envs per workgroup tile: 16, 32 or 64
 constexpr int kMinTileEnvs = 16;
+constexpr int kInvStride = 36;     // LDS bytes per inventory row (9 dwords: bank-spread)
 constexpr int kRecipeBytes = 12;  // compact recipe: out, ws, n_in, (kind, count) x 4, pad
 
 enum Mode { MODE_TICK = 0, MODE_TRANSITION = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
@@ -32,7 +34,6 @@ struct SimView {
   uint32_t* init;
   uint4* inv;
   uint4* mask;
-  const uint16_t* lut;        // [F]: feature f -> descriptor word | shift<<7 | wide<<12
   const uint16_t* task_tab;   // [n_tasks]: goal | arg_kind<<4 | n_subtasks<<12
   const int32_t* task_sub;    // [n_tasks][4] subtask ids
   int64_t* stats_part;        // [n_tiles][4]
@@ -40,37 +41,26 @@ struct SimView {
   int64_t n_envs, env_base;
   int32_t pool_count, n_tasks, n_recipes;
   int32_t W, H, K, F, C, CS, GS, maxT;
-  int32_t ND;                 // descriptor row stride in words (odd)
   int32_t bridge, axe;
+  int32_t obs_policy;         // observation stores: 0 write-back, 1 nontemporal, 2 write-through (sc1)
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
-  uint32_t magicQ;            // floor(2^32 / (F/4)) + 1
   const uint8_t* rc;          // [CRAFT_MAX_RECIPES][kRecipeBytes] compact recipes
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
 };
 
-// Observation descriptor of one env (LDS row, ND words):
-//   [0, w2)          local window cells as one-hot words (1 << kind, kind 0 dropped)
-//   [w2, 2w2)        block-max-pooled big-window kind masks
-//   2w2              1 << dir
-//   2w2 + 1          0 (the trailing constant feature)
-//   2w2 + 2 .. +9    inventory counts, 4 per word (the bytes transition() edits)
-// features() row f = (desc[lut.word] >> lut.shift) & (lut.wide ? 0xff : 1).
-__host__ __device__ constexpr int desc_dir_word(int win) { return 2 * win * win; }
-__host__ __device__ constexpr int desc_inv_word(int win) { return 2 * win * win + 2; }
-__host__ __device__ constexpr int desc_words(int win) { return 2 * win * win + 10; }
-
 // Dynamic-LDS carve of a tile workgroup (16-byte aligned pieces, Guideline 17):
-// grid rows [tile][GS] | descriptors [tile][ND] u32 | feature LUT [F] u16 |
-// task table [64] u16 | recipes [16][12] | agent words [tile] u32.
+// grid rows [tile][GS] | observation bytes [tile * F] (contiguous rows) |
+// inventory rows [tile][36] | task table [64] u16 | recipes [16][12] |
+// agent words [tile] u32.
 struct LdsLayout {
-  int desc, lut, task, rc, agent, bytes;
+  int obs, inv, task, rc, agent, bytes;
 };
-__host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int ND, int F) {
+__host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   LdsLayout l;
-  l.desc = up16(tile * GS);
-  l.lut = up16(l.desc + tile * ND * 4);
-  l.task = up16(l.lut + (F + 4) * 2);
+  l.obs = up16(tile * GS);
+  l.inv = up16(l.obs + tile * F);
+  l.task = up16(l.inv + tile * kInvStride);
   l.rc = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.agent = up16(l.rc + CRAFT_MAX_RECIPES * kRecipeBytes);
   l.bytes = up16(l.agent + tile * 4);

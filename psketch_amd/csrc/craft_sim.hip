@@ -114,14 +114,13 @@ struct craft_sim {
   uint32_t* d_init = nullptr;
   uint4* d_inv = nullptr;
   uint4* d_mask = nullptr;
-  uint16_t* d_lut = nullptr;
   uint16_t* d_task = nullptr;
   int32_t* d_task_sub = nullptr;
   uint8_t* d_rc = nullptr;
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   SimView view{};
-  int tile = craft::kMaxTileEnvs;   // envs per workgroup of the tick / observe kernels
+  int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
   int resident_cap = 0;             // 0: no cap on tile workgroups per CU
   std::string last_error;
 };
@@ -188,23 +187,6 @@ int validate_config(const craft_config_t* c, std::string& msg) {
   return CRAFT_OK;
 }
 
-// Feature index -> descriptor lookup (craft_device.h), in the layout of
-// CraftState.features (craft.py:296-330): local one-hot, pooled one-hot,
-// inventory counts, dir one-hot, trailing 0.
-std::vector<uint16_t> build_lut(const craft_config_t* c) {
-  const int w = c->window_width, K = c->n_kinds, W2 = w * w, L = W2 * K;
-  std::vector<uint16_t> lut((size_t)c->n_features + 4, 0);
-  auto enc = [](int word, int shift, int wide) { return (uint16_t)(word | (shift << 7) | (wide << 12)); };
-  for (int f = 0; f < c->n_features; ++f) {
-    if (f < L) lut[f] = enc(f / K, f % K, 0);
-    else if (f < 2 * L) lut[f] = enc(W2 + (f - L) / K, (f - L) % K, 0);
-    else if (f < 2 * L + K) { const int k = f - 2 * L; lut[f] = enc(craft::desc_inv_word(w) + k / 4, 8 * (k % 4), 1); }
-    else if (f < 2 * L + K + 4) lut[f] = enc(craft::desc_dir_word(w), f - 2 * L - K, 0);
-    else lut[f] = enc(craft::desc_dir_word(w) + 1, 0, 0);
-  }
-  return lut;
-}
-
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // LDS bytes per tile workgroup; a residency cap R pads the request to 160 KiB / R
@@ -212,7 +194,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // earlier tiles' observation stores.
 size_t lds_bytes(const craft_sim* s, int tile) {
   const SimView& v = s->view;
-  size_t b = (size_t)craft::lds_layout(tile, v.GS, v.ND, v.F).bytes;
+  size_t b = (size_t)craft::lds_layout(tile, v.GS, v.F).bytes;
   if (s->resident_cap > 0) {
     const size_t capped = ((size_t)163840 / s->resident_cap) & ~size_t(15);
     if (capped > b) b = capped;
@@ -221,8 +203,7 @@ size_t lds_bytes(const craft_sim* s, int tile) {
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
-  const int tile = (mode == craft::MODE_TICK || mode == craft::MODE_OBSERVE) ? s->tile : craft::kMaxTileEnvs;
-  hipError_t e = craft::launch_tile(mode, s->cfg.window_width, tile, s->view, a, lds_bytes(s, tile),
+  hipError_t e = craft::launch_tile(mode, s->cfg.window_width, s->tile, s->view, a, lds_bytes(s, s->tile),
                                     reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, what);
   return CRAFT_OK;
@@ -264,12 +245,11 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   s->env_base = env_id_base;
   s->pool_capacity = pool_capacity;
   s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs;   // stats rows
+  // default tile: the observation rows staged in LDS stay near 40 KB per workgroup
+  s->tile = cfg->window_width == 3 ? 64 : (cfg->window_width == 5 ? 32 : 16);
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
-  const int ww = cfg->window_width;
-  const int ND = craft::desc_words(ww) | 1;
-  std::vector<uint16_t> lut = build_lut(cfg);
   std::vector<uint8_t> rcb(CRAFT_MAX_RECIPES * craft::kRecipeBytes, 0);
   for (int r = 0; r < cfg->n_recipes; ++r) {
     const craft_recipe_t& rc = cfg->recipe[r];
@@ -306,15 +286,12 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_init, sizeof(uint32_t) * n_envs);
   ALLOC(s->d_inv, 2 * sizeof(uint4) * n_envs);
   ALLOC(s->d_mask, 2 * sizeof(uint4) * n_envs);
-  ALLOC(s->d_lut, sizeof(uint16_t) * lut.size());
   ALLOC(s->d_task, sizeof(uint16_t) * task_tab.size());
   ALLOC(s->d_task_sub, sizeof(int32_t) * task_sub.size());
   ALLOC(s->d_rc, rcb.size());
   ALLOC(s->d_stats, 4 * sizeof(int64_t) * s->n_tiles);
   ALLOC(s->d_err, 4 * sizeof(int32_t));
 #undef ALLOC
-  if ((e = hipMemcpy(s->d_lut, lut.data(), sizeof(uint16_t) * lut.size(), hipMemcpyHostToDevice)) != hipSuccess)
-    return cleanup(e, "lut");
   if ((e = hipMemcpy(s->d_task, task_tab.data(), sizeof(uint16_t) * task_tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "task table");
   if ((e = hipMemcpy(s->d_rc, rcb.data(), rcb.size(), hipMemcpyHostToDevice)) != hipSuccess)
@@ -328,7 +305,6 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.init = s->d_init;
   v.inv = s->d_inv;
   v.mask = s->d_mask;
-  v.lut = s->d_lut;
   v.task_tab = s->d_task;
   v.task_sub = s->d_task_sub;
   v.stats_part = s->d_stats;
@@ -340,8 +316,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.n_recipes = cfg->n_recipes;
   v.W = W; v.H = H; v.K = K; v.F = F; v.C = C; v.CS = CS; v.GS = GS;
   v.maxT = cfg->max_timesteps;
-  v.ND = ND;
   v.bridge = cfg->bridge_kind;
+  v.obs_policy = 1;   // nontemporal observation stores (fastest in tools/sweep_tiles.py)
   v.axe = cfg->axe_kind;
   v.kc_lo = v.kc_hi = 0;
   for (int k = 0; k < CRAFT_MAX_KINDS; ++k) {
@@ -349,21 +325,23 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     if (k < 16) v.kc_lo |= cls << (4 * k);
     else v.kc_hi |= cls << (4 * (k - 16));
   }
-  v.magicQ = (uint32_t)((1ull << 32) / (uint64_t)(F / 4 > 0 ? F / 4 : 1)) + 1u;
   v.rc = s->d_rc;
   *out = s;
   return CRAFT_OK;
 }
 
-int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_cu) {
+int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_cu, int32_t obs_store) {
   if (!s) return CRAFT_EINVAL;
-  if (tile_envs == 0) tile_envs = craft::kMaxTileEnvs;
+  if (tile_envs == 0) tile_envs = s->cfg.window_width == 3 ? 64 : (s->cfg.window_width == 5 ? 32 : 16);
   if (tile_envs != 16 && tile_envs != 32 && tile_envs != 64)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune: tile_envs must be 16, 32 or 64");
   if (max_resident_per_cu != 0 && (max_resident_per_cu < 3 || max_resident_per_cu > 32))
     return fail(s, CRAFT_EINVAL, "craft_sim_tune: max_resident_per_cu must be 0 or 3..32");
+  if (obs_store < 0 || obs_store > 2)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune: obs_store must be 0 (write-back), 1 (nontemporal) or 2 (write-through)");
   s->tile = tile_envs;
   s->resident_cap = max_resident_per_cu;
+  s->view.obs_policy = obs_store;
   return CRAFT_OK;
 }
 
@@ -375,7 +353,6 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_init);
   (void)hipFree(s->d_inv);
   (void)hipFree(s->d_mask);
-  (void)hipFree(s->d_lut);
   (void)hipFree(s->d_task);
   (void)hipFree(s->d_task_sub);
   (void)hipFree(s->d_rc);

@@ -1,31 +1,31 @@
 // craft_tile.hip — the hot kernel: one rollout tick (or transition / observe /
-// reset) for a tile of 64 consecutive envs per 256-thread workgroup.
+// reset) for a tile of TILE consecutive envs per 256-thread workgroup.
 //
-//   A  lanes 0..63 load their env's packed state, inventory and cleared-cell
-//      mask (one HBM round trip); the other waves stage the feature LUT and
-//      the task table into LDS.
-//   B  all threads copy the tile's 64 scenario grids from the (L2-resident)
-//      pool into LDS with coalesced dword loads.
-//   C  wave 0, one lane per env: clear masked cells, run the rollout protocol
-//      and CraftState.step on the LDS grid, write the state back, and leave
-//      inventory / dir / agent position in the env's LDS descriptor row.
-//   D  all 256 threads build the observation descriptor: local-window cell
-//      one-hots and block-max-pooled kind masks (independent LDS reads).
-//   E  all threads stream the tile's 64 x F fp32 observation rows to HBM as
-//      contiguous 16-byte stores; each value is one LDS word, shift and mask
-//      through the per-feature LUT (no branches).
-// The kernel is bound by E's HBM writes (F*4 = 1616 B per env at w=3); A-D
-// are a short latency chain.
+//   A  wave 0, one lane per env: load the env's packed state word, inventory,
+//      cleared-cell mask, restart spec and action (one HBM round trip), then its
+//      scenario row from the L2-resident pool, straight into LDS; the static
+//      task / recipe tables come along.  No workgroup barrier.
+//   C  same lanes: run the rollout protocol and CraftState.step on the LDS grid,
+//      write the state back.  Meanwhile waves 1-3 zero the tile's observation
+//      bytes in LDS.
+//   D  all threads scatter the observation's non-zero bytes (local-window
+//      one-hots, block-max-pooled one-hots, inventory counts, dir one-hot) into
+//      the tile's u8 rows [TILE][F] in LDS.
+//   E  all threads stream the rows to HBM as fp32: flat index s, one ds_read_b32
+//      of 4 feature bytes, 4 v_cvt_f32_ubyte, one contiguous 16-byte store.
+// The kernel is bound by E's HBM writes (F*4 = 1616 B per env at w=3).  See
+// DESIGN.md for the roofline and the phase timings that shaped this layout.
 #include "craft_device.h"
 
 namespace craft {
 
 #ifdef CRAFT_STAMPS
-// Diagnostic build only (never the product): wave 0 of every workgroup records
-// s_memrealtime (100 MHz) at phase boundaries into v.stamps[block][8].
+// Diagnostic build only (never the product): thread 0 of every workgroup
+// records s_memrealtime (100 MHz) at phase boundaries into v.stamps[block][8].
 #define STAMP(k)                                                                         \
   do {                                                                                   \
-    if (threadIdx.x == 0 && v.stamps) v.stamps[8 * (int64_t)blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0 && v.stamps)                                                    \
+      v.stamps[8 * (int64_t)blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();        \
   } while (0)
 #define STAMP_END()                                                                      \
   do {                                                                                   \
@@ -42,7 +42,10 @@ namespace craft {
 #define STAMP_END() do {} while (0)
 #endif
 
-template <int WIN>
+typedef unsigned int obs_vec __attribute__((ext_vector_type(4)));
+
+// Kind id at (cx, cy) of an LDS grid row as a one-hot bit, 0 outside the grid
+// (pad_slice's zero padding, misc/array.py:3-25).
 __device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int cx, int cy) {
   const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
   const int xc = min(max(cx, 0), W - 1), yc = min(max(cy, 0), H - 1);
@@ -51,40 +54,36 @@ __device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int
 }
 
 template <int WIN, int MODE, int TILE>
-__global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
-  constexpr int kTileEnvs = TILE;
-  constexpr int kThreads = 4 * TILE;
+__global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
+  constexpr int kParts = kThreads / TILE;        // threads per env in phase D
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const LdsLayout lay = lds_layout(TILE, v.GS, v.ND, v.F);
+  const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
   uint8_t* s_grid = smem;
-  uint32_t* s_desc = reinterpret_cast<uint32_t*>(smem + lay.desc);
-  uint16_t* s_lut = reinterpret_cast<uint16_t*>(smem + lay.lut);
+  uint8_t* s_obs = smem + lay.obs;
+  uint8_t* s_inv = smem + lay.inv;
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   uint8_t* s_rc = smem + lay.rc;
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
 
-  constexpr int kDirWord = desc_dir_word(WIN);
-  constexpr int kInvWord = desc_inv_word(WIN);
   const int tid = threadIdx.x;
-  const int64_t env0 = (int64_t)blockIdx.x * kTileEnvs;
-  const int nE = (int)min((int64_t)kTileEnvs, a.n - env0);
+  const int64_t env0 = (int64_t)blockIdx.x * TILE;
+  const int nE = (int)min((int64_t)TILE, a.n - env0);
   const bool want_obs = a.obs != nullptr;
+  const int F = v.F;
 
-  // ---- A+B: wave 0 loads each env's state, then its scenario row, and the static
-  //      tables; waves 1-3 stage the feature LUT (needed only in E). No barrier. -----
-  int64_t slot = 0, dslot = 0;
-  bool live = false;
-  uint32_t init_word = 0;
-  int act = 0;
-  uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0, m0 = i0, m1 = i0;
-  Agent s{};
   STAMP(0);
-  if (tid < kTileEnvs) {
-    // static tables: task entries and compact recipes (read by phase C)
-    if (tid < v.n_tasks) s_task[tid] = v.task_tab[tid];
-    if (tid < CRAFT_MAX_RECIPES * kRecipeBytes / 4)
-      reinterpret_cast<uint32_t*>(s_rc)[tid] = reinterpret_cast<const uint32_t*>(v.rc)[tid];
-    live = tid < nE;
+  // ---- A + C: wave 0, one lane per env ------------------------------------------------------
+  if (tid < TILE) {
+    for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
+    for (int t = tid; t < CRAFT_MAX_RECIPES * kRecipeBytes / 4; t += TILE)
+      reinterpret_cast<uint32_t*>(s_rc)[t] = reinterpret_cast<const uint32_t*>(v.rc)[t];
+
+    int64_t slot = 0, dslot = 0;
+    bool live = tid < nE;
+    uint32_t init_word = 0;
+    int act = 0;
+    uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0, m0 = i0, m1 = i0;
+    Agent s{};
     if (live) {
       const int64_t i = env0 + tid;
       slot = (MODE == MODE_TICK || MODE == MODE_RESET || !a.src) ? i : (int64_t)a.src[i];
@@ -97,7 +96,7 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
     if (live) {
       if (MODE == MODE_RESET) {
         const int64_t i = env0 + tid;
-        int sc = a.r_scen[i], x0 = a.r_x[i], y0 = a.r_y[i], d0 = a.r_dir[i], tk = a.r_task[i];
+        const int sc = a.r_scen[i], x0 = a.r_x[i], y0 = a.r_y[i], d0 = a.r_dir[i], tk = a.r_task[i];
         if (sc < 0 || sc >= v.pool_count || x0 < 1 || x0 > v.W - 2 || y0 < 1 || y0 > v.H - 2 ||
             d0 < 0 || d0 > 3 || tk < 0 || tk >= v.n_tasks) {
           latch_error(v.err, CRAFT_EINVAL, i);
@@ -129,10 +128,11 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
         }
       }
     }
+    uint8_t* g = s_grid + tid * v.GS;
     if (live) {
       // the env's scenario grid: CS/16 independent 16-byte loads (L2-resident pool)
       const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
-      uint32_t* dst = reinterpret_cast<uint32_t*>(s_grid + tid * v.GS);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(g);
       const int nchunk = v.CS >> 4;
       uint4 c[CRAFT_MAX_CELLS / 16];
 #pragma unroll
@@ -144,32 +144,24 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
           dst[4 * q + 0] = c[q].x; dst[4 * q + 1] = c[q].y; dst[4 * q + 2] = c[q].z; dst[4 * q + 3] = c[q].w;
         }
     }
-    // LDS written above is read below only by the same lane or, for the tables, by
-    // lanes of this same wave: order the wave's LDS accesses, no workgroup barrier.
+    // Every LDS word written above is read below by the same lane, or (the
+    // tables) by lanes of this same wave: order the wave's LDS accesses.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  } else if (want_obs) {
-    const uint32_t* lut32 = reinterpret_cast<const uint32_t*>(v.lut);
-    uint32_t* s_lut32 = reinterpret_cast<uint32_t*>(s_lut);
-    for (int w = tid - kTileEnvs; w < (v.F + 1) / 2; w += kThreads - kTileEnvs) s_lut32[w] = lut32[w];
-  }
-  STAMP(2);
+    STAMP(1);
 
-  // ---- C: one lane per env -------------------------------------------------------------
-  if (tid < kTileEnvs) {
-    uint8_t* g = s_grid + tid * v.GS;
-    uint32_t* row = s_desc + tid * v.ND;
-    uint8_t* iv = reinterpret_cast<uint8_t*>(row + kInvWord);
+    // ---- C ----
+    uint32_t* ivw = reinterpret_cast<uint32_t*>(s_inv + tid * kInvStride);
+    uint8_t* iv = s_inv + tid * kInvStride;
     uint32_t m[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-    row[kInvWord + 0] = i0.x; row[kInvWord + 1] = i0.y; row[kInvWord + 2] = i0.z; row[kInvWord + 3] = i0.w;
-    row[kInvWord + 4] = i1.x; row[kInvWord + 5] = i1.y; row[kInvWord + 6] = i1.z; row[kInvWord + 7] = i1.w;
+    ivw[0] = i0.x; ivw[1] = i0.y; ivw[2] = i0.z; ivw[3] = i0.w;
+    ivw[4] = i1.x; ivw[5] = i1.y; ivw[6] = i1.z; ivw[7] = i1.w;
     bool inv_changed = false, mask_changed = false;
     int d = 0, succ = -1, counted = 0;
     if (live) {
       // The LDS row holds pool[scenario]; cells cleared this episode are applied
-      // lazily so that an auto-reset (which restores exactly that row) needs no
-      // global reload.
+      // lazily, so an auto-reset (which restores exactly that row) needs no reload.
       bool restart = false;
       if (MODE == MODE_TICK) {
         // per-env body of ImitationTrainer.do_rollout, trainers/imitation.py:59-73
@@ -182,7 +174,7 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
           restart = d && (a.flags & CRAFT_STEP_AUTORESET);
         }
         if (d) {
-          // satisfies() on the pre-step state: only the facing cell and the inventory matter
+          // satisfies() of the pre-step state: only the facing cell and the inventory matter
           const uint32_t tt = s_task[s.task];
           const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));
           uint32_t mw = 0;
@@ -211,7 +203,7 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
           s.x = init_word & 0xff; s.y = (init_word >> 8) & 0xff; s.dir = (init_word >> 16) & 3;
           s.timer = v.maxT;
 #pragma unroll
-          for (int w = 0; w < 8; ++w) { row[kInvWord + w] = 0u; m[w] = 0u; }
+          for (int w = 0; w < 8; ++w) { ivw[w] = 0u; m[w] = 0u; }
           inv_changed = mask_changed = true;
         } else if (d && !s.frozen) {
           s.frozen = 1;
@@ -240,8 +232,8 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
       if (MODE == MODE_RESET) v.init[dslot] = (uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16);
       if (MODE == MODE_TRANSITION && dslot != slot) v.init[dslot] = init_word;
       if (inv_changed) {
-        v.inv[2 * dslot] = make_uint4(row[kInvWord], row[kInvWord + 1], row[kInvWord + 2], row[kInvWord + 3]);
-        v.inv[2 * dslot + 1] = make_uint4(row[kInvWord + 4], row[kInvWord + 5], row[kInvWord + 6], row[kInvWord + 7]);
+        v.inv[2 * dslot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+        v.inv[2 * dslot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
       }
       if (mask_changed) {
         v.mask[2 * dslot] = make_uint4(m[0], m[1], m[2], m[3]);
@@ -253,13 +245,8 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
         if (a.sat) a.sat[i] = (int8_t)succ;
         if (a.reward) a.reward[i] = (counted && d && succ == 1) ? 1.0f : 0.0f;
       }
-    } else if (want_obs) {
-#pragma unroll
-      for (int w = 0; w < 8; ++w) row[kInvWord + w] = 0u;
     }
-    row[kDirWord] = live ? (1u << s.dir) : 0u;
-    row[kDirWord + 1] = 0u;
-    s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | (1u << 16)) : 0u;
+    s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
     if (MODE == MODE_TICK) {
       // episode statistics: one partial-sum row per workgroup (uncontended)
       const uint64_t bs = __ballot(live && counted && d && succ == 1);
@@ -272,6 +259,11 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
         atomicAdd(r + 2, (unsigned long long)__popcll(bt));
       }
     }
+  } else if (want_obs) {
+    // waves 1-3: zero the tile's observation bytes while wave 0 runs A + C
+    uint4* z = reinterpret_cast<uint4*>(s_obs);
+    const int n16 = (nE * F + 15) >> 4;
+    for (int i = tid - TILE; i < n16; i += kThreads - TILE) z[i] = make_uint4(0, 0, 0, 0);
   }
   STAMP(3);
   if (!want_obs) {
@@ -281,70 +273,93 @@ __global__ __launch_bounds__(4 * TILE) void tile_kernel(SimView v, TileArgs a) {
   __syncthreads();
   STAMP(4);
 
-  // ---- D: descriptors (local one-hots, pooled kind masks), all threads -----------------
+  // ---- D: scatter the observation's non-zero bytes ---------------------------------------------
   {
-    const int e = tid & (kTileEnvs - 1), part = tid / kTileEnvs;
+    const int e = tid % TILE, part = tid / TILE;
     const uint32_t ag = s_agent[e];
-    uint32_t* row = s_desc + e * v.ND;
-    const uint8_t* g = s_grid + e * v.GS;
-    const int W = v.W, H = v.H;
-    const int x = ag & 0xff, y = (ag >> 8) & 0xff;
-    const bool ok = (ag >> 16) & 1;
-    constexpr int W2 = WIN * WIN;
-    if (part == 0) {
-      constexpr int hw = WIN / 2;
+    if (e < nE && (ag >> 24)) {
+      const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+      const uint8_t* g = s_grid + e * v.GS;
+      uint8_t* row = s_obs + e * F;
+      const int W = v.W, H = v.H, K = v.K;
+      constexpr int W2 = WIN * WIN;
+      const int L = W2 * K;
+      if (part == 0) {
+        constexpr int hw = WIN / 2;
 #pragma unroll
-      for (int i = 0; i < WIN; ++i)
+        for (int i = 0; i < WIN; ++i)
 #pragma unroll
-        for (int j = 0; j < WIN; ++j)
-          row[i * WIN + j] = ok ? (cell_bit<WIN>(g, W, H, x - hw + i, y - hw + j) & ~1u) : 0u;
-    } else {
-      constexpr int bh = W2 / 2;
+          for (int j = 0; j < WIN; ++j) {
+            const int cx = x - hw + i, cy = y - hw + j;
+            if ((unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H) {
+              const int k = g[cx * H + cy];
+              if (k) row[(i * WIN + j) * K + k] = 1;                   // local one-hot
+            }
+          }
+        const uint8_t* iv = s_inv + e * kInvStride;
+        for (int k = 0; k < K; ++k) row[2 * L + k] = iv[k];           // inventory counts
+        row[2 * L + K + dir] = 1;                                      // dir one-hot
+      } else {
+        constexpr int bh = W2 / 2;
 #pragma unroll
-      for (int j = 0; j < (W2 + 2) / 3; ++j) {
-        const int b = part - 1 + 3 * j;
-        if (b >= W2) break;
-        const int bi = b / WIN, bj = b - bi * WIN;
-        const int x0 = x - bh + bi * WIN, y0 = y - bh + bj * WIN;
-        uint32_t msk = 0;
-        if (ok && x0 < W && x0 + WIN > 0 && y0 < H && y0 + WIN > 0) {
+        for (int j = 0; j < (W2 + kParts - 2) / (kParts - 1); ++j) {
+          const int b = part - 1 + (kParts - 1) * j;
+          if (b >= W2) break;
+          const int bi = b / WIN, bj = b - bi * WIN;
+          const int x0 = x - bh + bi * WIN, y0 = y - bh + bj * WIN;
+          uint32_t msk = 0;
+          if (x0 < W && x0 + WIN > 0 && y0 < H && y0 + WIN > 0) {
 #pragma unroll
-          for (int ii = 0; ii < WIN; ++ii)
+            for (int ii = 0; ii < WIN; ++ii)
 #pragma unroll
-            for (int jj = 0; jj < WIN; ++jj) msk |= cell_bit<WIN>(g, W, H, x0 + ii, y0 + jj);
+              for (int jj = 0; jj < WIN; ++jj) msk |= cell_bit(g, W, H, x0 + ii, y0 + jj);
+          }
+          msk &= ~1u;                                                  // kind 0 = empty
+          uint8_t* brow = row + L + b * K;
+          while (msk) {                                                // block-max-pooled one-hot
+            brow[__ffs(msk) - 1] = 1;
+            msk &= msk - 1;
+          }
         }
-        row[W2 + b] = msk & ~1u;
       }
     }
   }
   __syncthreads();
   STAMP(5);
 
-  // ---- E: stream the tile's observation rows --------------------------------------------
-  const int F = v.F;
-  float* tile = a.obs + env0 * (int64_t)F;
-  if ((F & 3) == 0) {
-    const int Q = F >> 2;
-    const int nslots = nE * Q;
-    float4* out4 = reinterpret_cast<float4*>(tile);
-    for (int sidx = tid; sidx < nslots; sidx += kThreads) {
-      const int e = (int)__umulhi((uint32_t)sidx, v.magicQ);
-      const int f = (sidx - e * Q) << 2;
-      const uint2 lw = *reinterpret_cast<const uint2*>(s_lut + f);
-      const uint32_t* row = s_desc + e * v.ND;
-      const uint32_t u0 = lw.x & 0xffff, u1 = lw.x >> 16, u2 = lw.y & 0xffff, u3 = lw.y >> 16;
-      float4 o;
-      o.x = (float)((row[u0 & 127] >> ((u0 >> 7) & 31)) & ((u0 & 4096) ? 0xffu : 1u));
-      o.y = (float)((row[u1 & 127] >> ((u1 >> 7) & 31)) & ((u1 & 4096) ? 0xffu : 1u));
-      o.z = (float)((row[u2 & 127] >> ((u2 >> 7) & 31)) & ((u2 & 4096) ? 0xffu : 1u));
-      o.w = (float)((row[u3 & 127] >> ((u3 >> 7) & 31)) & ((u3 & 4096) ? 0xffu : 1u));
-      out4[sidx] = o;
+  // ---- E: stream the tile's rows to HBM as fp32 ------------------------------------------------
+  {
+    const int total = nE * F;                  // floats in this tile (rows are contiguous)
+    const int n4 = total >> 2;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(s_obs);
+    float* tile_out = a.obs + env0 * (int64_t)F;
+    // Buffer stores: 32-bit offsets off one wave-uniform descriptor; the cache
+    // policy of the observation stream is a tuning knob (craft_sim_tune).
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * 4, 0x00020000);
+    constexpr int U = 4;                       // independent 16-byte stores in flight per lane
+    for (int base = tid; base < n4; base += U * kThreads) {
+      uint32_t w[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int sidx = base + u * kThreads;
+        w[u] = sidx < n4 ? src[sidx] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int sidx = base + u * kThreads;
+        if (sidx < n4) {
+          const float4 f = make_float4((float)(w[u] & 0xff), (float)((w[u] >> 8) & 0xff),   // v_cvt_f32_ubyte0..3
+                                       (float)((w[u] >> 16) & 0xff), (float)(w[u] >> 24));
+          const obs_vec o = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
+          if (v.obs_policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, sidx * 16, 0, 2);         // nt
+          else if (v.obs_policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, sidx * 16, 0, 16);   // sc1
+          else __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, sidx * 16, 0, 0);
+        }
+      }
     }
-  } else {
-    for (int sidx = tid; sidx < nE * F; sidx += kThreads) {
-      const int e = sidx / F, f = sidx - e * F;
-      const uint32_t u = s_lut[f];
-      tile[sidx] = (float)((s_desc[e * v.ND + (u & 127)] >> ((u >> 7) & 31)) & ((u & 4096) ? 0xffu : 1u));
+    if (tid < (total & 3)) {                   // F % 4 != 0: the last few floats
+      const int f = (n4 << 2) + tid;
+      a.obs[env0 * (int64_t)F + f] = (float)s_obs[f];
     }
   }
   STAMP_END();
@@ -354,7 +369,7 @@ template <int WIN, int MODE, int TILE>
 static hipError_t launch_one(const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
   const int64_t tiles = (a.n + TILE - 1) / TILE;
   if (tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL((tile_kernel<WIN, MODE, TILE>), dim3((unsigned)tiles), dim3(4 * TILE), lds, st, v, a);
+  hipLaunchKernelGGL((tile_kernel<WIN, MODE, TILE>), dim3((unsigned)tiles), dim3(kThreads), lds, st, v, a);
   return hipGetLastError();
 }
 
@@ -377,15 +392,13 @@ static hipError_t launch_tiled(int tile, int win, const SimView& v, const TileAr
   }
 }
 
-// The rollout tick and the observation take the tuned tile size; the
-// reference-granular transition / reset always run 64-env tiles.
 hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
                        hipStream_t st) {
   switch (mode) {
     case MODE_TICK: return launch_tiled<MODE_TICK>(tile, win, v, a, lds, st);
     case MODE_OBSERVE: return launch_tiled<MODE_OBSERVE>(tile, win, v, a, lds, st);
-    case MODE_TRANSITION: return launch_win<MODE_TRANSITION, 64>(win, v, a, lds, st);
-    default: return launch_win<MODE_RESET, 64>(win, v, a, lds, st);
+    case MODE_TRANSITION: return launch_tiled<MODE_TRANSITION>(tile, win, v, a, lds, st);
+    default: return launch_tiled<MODE_RESET>(tile, win, v, a, lds, st);
   }
 }
 

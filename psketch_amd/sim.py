@@ -73,10 +73,11 @@ class CraftSim:
         except Exception:
             pass
 
-    def tune(self, tile_envs=0, max_resident_per_cu=0):
-        """Tick/observe kernel geometry (results are identical for every setting)."""
-        self._check(N.lib().craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu)),
-                    "craft_sim_tune")
+    def tune(self, tile_envs=0, max_resident_per_cu=0, obs_store=0):
+        """Tile-kernel geometry and observation-store cache policy (0 write-back,
+        1 nontemporal, 2 write-through); results are identical for every setting."""
+        self._check(N.lib().craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu),
+                                           int(obs_store)), "craft_sim_tune")
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

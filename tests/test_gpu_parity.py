@@ -318,9 +318,9 @@ def test_tuning_does_not_change_results(window):
     n = 5000   # not a multiple of any tile: exercises the partial last tile
     specs = synthetic_specs(pool, 12, 12, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
     ref = None
-    for tile, cap in [(64, 0), (32, 0), (16, 0), (16, 6), (32, 4), (64, 3)]:
+    for tile, cap, pol in [(64, 0, 0), (32, 0, 1), (16, 0, 2), (16, 6, 0), (32, 4, 2), (64, 3, 1)]:
         sim = sim_with_pool(world, n, pool)
-        sim.tune(tile, cap)
+        sim.tune(tile, cap, pol)
         sim.reset(*specs)
         obs = sim.empty_obs()
         outs = []

@@ -37,14 +37,14 @@ def run(world, n=65536, ticks=20, obs=True):
         res.append(s[:, :7] - t0)
     r = np.stack(res[5:])                       # [ticks, tiles, 7]
     out = {"world": world, "obs": obs}
-    names = ["A", "B", "C", "D_wait", "D", "E"]
-    idx = [(0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6)] if obs else [(0, 1), (1, 2), (2, 3)]
+    names = ["A", "C", "D_wait", "D", "E"]
+    idx = [(0, 1), (1, 3), (3, 4), (4, 5), (5, 6)] if obs else [(0, 1), (1, 3)]
     for nm, (i, j) in zip(names, idx):
         d = r[:, :, j] - r[:, :, i]
-        out[nm + "_med"] = float(np.median(d))
-        out[nm + "_p90"] = float(np.percentile(d, 90))
+        out[nm + "_med"] = round(float(np.median(d)), 2)
+        out[nm + "_p90"] = round(float(np.percentile(d, 90)), 2)
     out["start_spread_p50_p100"] = [float(np.median(r[:, :, 0])), float(r[:, :, 0].max())]
-    last = 6 if obs else 3
+    last = 6
     out["end_p50"] = float(np.median(r[:, :, last]))
     out["end_max"] = float(np.median(r[:, :, last].max(axis=1)))
     out["xcc_hist"] = np.bincount(st[: (n + 63) // 64, 7].cpu().numpy().astype(np.int64), minlength=8).tolist()

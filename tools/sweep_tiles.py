@@ -25,13 +25,12 @@ for world in sys.argv[1:] or ["craft_medium_12x12"]:
     def step():
         sim.step(seed=0, tick=st["t"], obs=ring[st["t"] % 4]); st["t"] += 1
     res = {}
-    for tile in (16, 32, 64):
-        for cap in (0, 3, 4, 5, 6, 8, 12, 16):
-            if cap and cap * 4 * tile // 64 > 32:   # more waves than a CU holds: same as no cap
-                continue
-            sim.tune(tile, cap)
-            res[f"t{tile}_c{cap}"] = round(timeit(step), 2)
-    sim.tune(0, 0)
+    for pol in (0, 1, 2):
+        for tile in (32, 64):
+            for cap in (0, 4, 6):
+                sim.tune(tile, cap, pol)
+                res[f"p{pol}_t{tile}_c{cap}"] = round(timeit(step), 2)
+    sim.tune(0, 0, 1)
     sim.check()
     out[world] = dict(sorted(res.items(), key=lambda kv: kv[1]))
 print(json.dumps(out, indent=1))
