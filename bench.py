@@ -72,25 +72,21 @@ def cpu_baseline(sim, grids, specs, seconds):
 
 def main():
     args = parse()
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
+    from psketch_amd import distributed as D
+
+    rank, world_size, local_rank = D.world()
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    dist = None
-    if world_size > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    D.init(device=dev)                        # RCCL process group when WORLD_SIZE > 1
 
-    from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
-
-    n = args.envs
-    sim = CraftSim(args.world, n_envs=n, device=local_rank, env_id_base=rank * n,
+    env_base, n = D.env_shard(rank, args.envs)
+    sim = CraftSim(args.world, n_envs=n, device=local_rank, env_id_base=env_base,
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
-    specs = synthetic_specs(grids, sim.width, sim.height, n, rank * n, seed=args.seed,
+    specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
                             task_ids=tasks)
     sim.reset(*specs)
     F = sim.n_features
@@ -112,8 +108,7 @@ def main():
     sim.check()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        D.barrier()
         torch.cuda.synchronize()
 
     # ---- timed region: K ticks, barrier + synchronize on both sides ------------------
@@ -122,11 +117,7 @@ def main():
     for _ in range(args.steps):
         step()
     barrier()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
 
     # ---- per-launch kernel duration, HIP events on the launch stream --------------------
     kstream = torch.cuda.current_stream(dev)
@@ -142,10 +133,7 @@ def main():
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
     # ---- scalar episode summary: one RCCL all-reduce of int64[3] --------------------------
-    stats = sim.stats()
-    if dist is not None:
-        dist.all_reduce(stats)
-    stats = stats.cpu().tolist()
+    stats = D.reduce_episode_stats(sim.stats()).cpu().tolist()
     sim.check()
 
     if rank == 0:
@@ -191,9 +179,7 @@ def main():
         if world_size == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sim, grids, specs, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    D.shutdown()
 
 
 if __name__ == "__main__":
