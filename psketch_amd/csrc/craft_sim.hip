@@ -487,7 +487,7 @@ int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
   if (4 * s->view.C > 1000)
     return fail(s, CRAFT_EINVAL, "craft_teacher: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
   if (n == 0) return CRAFT_OK;
-  hipError_t e = craft::launch_teacher((s->view.C + 63) / 64, s->view, slots, tasks, n, action_out,
+  hipError_t e = craft::launch_teacher((s->view.C + 31) / 32, s->view, slots, tasks, n, action_out,
                                        path_len_out, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_teacher launch");
   return CRAFT_OK;

@@ -5,16 +5,18 @@
 
 namespace craft {
 
+// A set of cells as NW 32-bit words (cell c = bit c & 31 of word c >> 5).
+// Multi-word shifts use v_alignbit_b32 (one funnel shift per word).
 template <int NW>
 struct Bits {
-  uint64_t w[NW];
+  uint32_t w[NW];
 };
 
 template <int NW>
 __device__ __forceinline__ Bits<NW> bzero() {
   Bits<NW> r;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = 0;
+  for (int i = 0; i < NW; ++i) r.w[i] = 0u;
   return r;
 }
 template <int NW>
@@ -40,23 +42,23 @@ __device__ __forceinline__ Bits<NW> bandn(const Bits<NW>& a, const Bits<NW>& b) 
 }
 template <int NW>
 __device__ __forceinline__ bool bany(const Bits<NW>& a) {
-  uint64_t x = 0;
+  uint32_t x = 0;
 #pragma unroll
   for (int i = 0; i < NW; ++i) x |= a.w[i];
-  return x != 0;
+  return x != 0u;
 }
 template <int NW>
 __device__ __forceinline__ bool btest(const Bits<NW>& a, int p) {
-  uint64_t x = 0;
+  uint32_t x = 0;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) x |= (i == (p >> 6)) ? a.w[i] : 0ull;
-  return (x >> (p & 63)) & 1ull;
+  for (int i = 0; i < NW; ++i) x |= (i == (p >> 5)) ? a.w[i] : 0u;
+  return (x >> (p & 31)) & 1u;
 }
 template <int NW>
 __device__ __forceinline__ Bits<NW> bbit(int p) {
   Bits<NW> r;
 #pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = (i == (p >> 6)) ? (1ull << (p & 63)) : 0ull;
+  for (int i = 0; i < NW; ++i) r.w[i] = (i == (p >> 5)) ? (1u << (p & 31)) : 0u;
   return r;
 }
 template <int NW>
@@ -64,7 +66,7 @@ __device__ __forceinline__ int blowest(const Bits<NW>& a) {   // INT_MAX if empt
   int r = INT_MAX;
 #pragma unroll
   for (int i = NW - 1; i >= 0; --i)
-    if (a.w[i]) r = i * 64 + __ffsll((unsigned long long)a.w[i]) - 1;
+    if (a.w[i]) r = i * 32 + __ffs(a.w[i]) - 1;
   return r;
 }
 template <int NW>
@@ -72,21 +74,22 @@ __device__ __forceinline__ int bhighest(const Bits<NW>& a) {  // -1 if empty
   int r = -1;
 #pragma unroll
   for (int i = 0; i < NW; ++i)
-    if (a.w[i]) r = i * 64 + 63 - __clzll((long long)a.w[i]);
+    if (a.w[i]) r = i * 32 + 31 - __clz(a.w[i]);
   return r;
 }
-// p -> p + d for every member (|d| < 64); members shifted past either end drop out.
+// p -> p + d for every member (0 < |d| < 32); members shifted past either end drop out.
 template <int NW>
 __device__ __forceinline__ Bits<NW> bshift(const Bits<NW>& a, int d) {
   Bits<NW> r;
   if (d > 0) {
+    r.w[0] = a.w[0] << d;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) r.w[i] = (a.w[i] << d) | (i > 0 ? a.w[i - 1] >> (64 - d) : 0ull);
+    for (int i = 1; i < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i], a.w[i - 1], 32 - d);
   } else {
     const int s = -d;
 #pragma unroll
-    for (int i = 0; i < NW; ++i)
-      r.w[i] = (a.w[i] >> s) | (i + 1 < NW ? a.w[i + 1] << (64 - s) : 0ull);
+    for (int i = 0; i + 1 < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i + 1], a.w[i], s);
+    r.w[NW - 1] = a.w[NW - 1] >> s;
   }
   return r;
 }
@@ -160,22 +163,22 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
       first_action = bl;
     }
     if (!bany(bandn(tgt, claimed))) break;
-    Bits<NW> nc[4], nf[4];
+    // Expand label by label, in place: a label's current set is only needed for
+    // its own expansion, and V[a] (updated immediately) gives smaller labels priority.
 #pragma unroll
     for (int lab = 0; lab < 4; ++lab) {
-      nc[lab] = bzero<NW>();
-      nf[lab] = bzero<NW>();
+      Bits<NW> nc = bzero<NW>(), nf = bzero<NW>();
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         const Bits<NW> moved = bor(band(bshift(cur[lab], dl[a]), fr), band(cur[lab], blk[a]));
         const Bits<NW> fresh = bandn(moved, V[a]);
         V[a] = bor(V[a], fresh);
-        nc[lab] = bor(nc[lab], fresh);
-        nf[lab] = bor(nf[lab], band(bshift(fresh, dl[a]), valid));
+        nc = bor(nc, fresh);
+        nf = bor(nf, band(bshift(fresh, dl[a]), valid));
       }
+      cur[lab] = nc;
+      fc[lab] = nf;
     }
-#pragma unroll
-    for (int lab = 0; lab < 4; ++lab) { cur[lab] = nc[lab]; fc[lab] = nf[lab]; }
     ++depth;
   }
   if (found) {
@@ -244,24 +247,40 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   Bits<NW> valid = bzero<NW>();
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
-    const int nb = min(64, max(0, C - w * 64));
-    valid.w[w] = nb >= 64 ? ~0ull : ((1ull << nb) - 1ull);
+    const int nb = min(32, max(0, C - w * 32));
+    valid.w[w] = nb >= 32 ? ~0u : ((1u << nb) - 1u);
   }
-  auto closest = [&](int kind, int& fa, int& len) -> bool {
-    Bits<NW> occ = bzero<NW>(), tgt = bzero<NW>();
-    for (int c = 0; c < C; ++c) {
-      const int k = grid_kind(v, s.scen, m, c);
-      if (k) {
+  // Occupancy and per-kind target bitsets of the current grid (pool row minus the
+  // cleared-cell mask): the row is read as dwords in a fully unrolled loop so every
+  // bit position is static (no per-cell dependent loads, no dynamic indexing).
+  const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
+  const int nq = (C + 3) >> 2;
+  auto grids = [&](int kind, Bits<NW>& occ, Bits<NW>& tgt) {
+    occ = bzero<NW>();
+    tgt = bzero<NW>();
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const uint64_t b = (w == (c >> 6)) ? (1ull << (c & 63)) : 0ull;
-          occ.w[w] |= b;
-          if (k == kind) tgt.w[w] |= b;
+    for (int q = 0; q < NW * 8; ++q) {
+      if (q < nq) {
+        const uint32_t w = row32[q];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int c = 4 * q + b;
+          const uint32_t k = (w >> (8 * b)) & 0xffu;
+          const bool cleared = (m[c >> 5] >> (c & 31)) & 1u;
+          const uint32_t bit = (k != 0 && !cleared) ? (1u << (c & 31)) : 0u;
+          occ.w[c >> 5] |= bit;
+          tgt.w[c >> 5] |= (k == (uint32_t)kind) ? bit : 0u;
         }
       }
     }
+  };
+  auto closest = [&](int kind, int& fa, int& len) -> bool {
+    Bits<NW> occ, tgt;
+    grids(kind, occ, tgt);
     return bfs_closest<NW>(occ, tgt, valid, H, s.x * H + s.y, s.dir, fa, len);
   };
+  int leaf_kind = -1, leaf_fa = -1, leaf_len = -1;
+  bool leaf_ok = true;
 
   int action = CRAFT_STOP;
   int err = 0;
@@ -286,7 +305,9 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
         action = CRAFT_USE;
       } else if (goal == CRAFT_GOAL_GO) {
         int fa = -1, len = -1;
-        if (!closest(arg, fa, len)) err = CRAFT_ETEACHER;
+        leaf_ok = closest(arg, fa, len);
+        leaf_kind = arg; leaf_fa = fa; leaf_len = len;
+        if (!leaf_ok) err = CRAFT_ETEACHER;
         else if (len < 0) action = CRAFT_STOP;                           // demonstration.py:25-26
         else if (len == 0) err = CRAFT_ETEACHER;                         // [][0]
         else action = fa;
@@ -302,8 +323,13 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   a.act_out[i] = action;
   if (a.len_out) {
     const int arg = (v.task_tab[task] >> 4) & 0xff;
-    int fa = -1, len = -1;
-    if (arg > 0 && !closest(arg, fa, len)) {
+    int fa = leaf_fa, len = leaf_len;
+    bool ok = leaf_ok;
+    if (arg != leaf_kind) {               // the teacher's BFS already answered get[X]'s go[X]
+      len = -1;
+      ok = arg > 0 ? closest(arg, fa, len) : true;
+    }
+    if (!ok) {
       latch_error(v.err, CRAFT_ETEACHER, slot);
       len = -2;
     }
@@ -315,12 +341,11 @@ hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const 
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
   TeachArgs a{slots, tasks, n, act_out, len_out};
   const unsigned blocks = (unsigned)((n + 255) / 256);
-  switch (nw) {
-    case 1: hipLaunchKernelGGL(teacher_kernel<1>, dim3(blocks), dim3(256), 0, st, v, a); break;
-    case 2: hipLaunchKernelGGL(teacher_kernel<2>, dim3(blocks), dim3(256), 0, st, v, a); break;
-    case 3: hipLaunchKernelGGL(teacher_kernel<3>, dim3(blocks), dim3(256), 0, st, v, a); break;
-    default: hipLaunchKernelGGL(teacher_kernel<4>, dim3(blocks), dim3(256), 0, st, v, a); break;
-  }
+  // nw = 32-bit words per cell set: 8x8 -> 2, 10x10 -> 4, 12x12 -> 5, 16x16 -> 8
+  if (nw <= 2) hipLaunchKernelGGL(teacher_kernel<2>, dim3(blocks), dim3(256), 0, st, v, a);
+  else if (nw <= 4) hipLaunchKernelGGL(teacher_kernel<4>, dim3(blocks), dim3(256), 0, st, v, a);
+  else if (nw <= 5) hipLaunchKernelGGL(teacher_kernel<5>, dim3(blocks), dim3(256), 0, st, v, a);
+  else hipLaunchKernelGGL(teacher_kernel<8>, dim3(blocks), dim3(256), 0, st, v, a);
   return hipGetLastError();
 }
 

@@ -68,6 +68,9 @@ WORLDS = {
                                N_WORKSHOPS=3, N_PRIMITIVES=2, N_WORLDS=100),
     "craft_medium_12x12_w5": dict(WIDTH=12, HEIGHT=12, WINDOW_WIDTH=5, WINDOW_HEIGHT=5,
                                   N_WORKSHOPS=3, N_PRIMITIVES=2, N_WORLDS=100),
+    # largest geometry the kernels support (W*H = 256, window 7): coverage only
+    "craft_16x16_w7": dict(WIDTH=16, HEIGHT=16, WINDOW_WIDTH=7, WINDOW_HEIGHT=7,
+                           N_WORKSHOPS=3, N_PRIMITIVES=4, N_WORLDS=100),
 }
 
 # trainer.max_timesteps, configs/experiments/imitation.yaml:21

@@ -341,3 +341,35 @@ def test_tuning_does_not_change_results(window):
             for k in st:
                 np.testing.assert_array_equal(st[k], ref[1][k])
             np.testing.assert_array_equal(stats, ref[2])
+
+
+@pytest.mark.parametrize("world,W", [("craft_medium", 8), ("craft_large", 10), ("craft_16x16_w7", 16)])
+def test_lockstep_other_geometries(oracle_mod, world, W):
+    """Other grid sizes / windows (row strides, pooled-window clipping, the
+    w=5 and w=7 kernels, 16x16 = 256 cells): 1024 envs x 60 ticks bit-exact."""
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 7, 64)
+    n = 1024
+    specs = synthetic_specs(pool, W, W, n, 0, seed=5, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    sim.reset(*specs)
+    o, envs = oracle_from_sim_specs(oracle_mod, cfg, pool, specs)
+    obs = sim.empty_obs()
+    done = torch.empty(n, dtype=torch.uint8, device="cuda")
+    succ = torch.empty(n, dtype=torch.int8, device="cuda")
+    for t in range(60):
+        sim.step(seed=8, tick=t, obs=obs, done=done, success=succ)
+        rc, oobs, _, odone, osucc = o.batch_tick(envs, 0, None, 8, t, True, True)
+        np.testing.assert_array_equal(host(obs), oobs, err_msg=f"t={t}")
+        np.testing.assert_array_equal(host(done), odone)
+        np.testing.assert_array_equal(host(succ), osucc)
+    st = sim.get_state()
+    np.testing.assert_array_equal(host(st["grid"]), envs["grid"][:, :W * W])
+    np.testing.assert_array_equal(host(st["inventory"]), envs["inv"][:, :cfg.n_kinds])
+    if 4 * W * W <= 1000:
+        act, _ = sim.teacher()
+        act = host(act)
+        for i in range(0, n, 3):
+            rc, a = o.teacher(envs[i:i + 1], int(specs[4][i]))
+            assert (a if rc == 0 else -2) == act[i], i
+    sim.check()
