@@ -222,7 +222,9 @@ int craft_observe(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32
  * len(best_action_seq) of find_closest_resources for the task's own goal_arg
  * (the trainer's `distances`, trainers/imitation.py:79-91), -1 if no target.
  * Where the reference raises (base.py:24 assert, base.py:31 len(None),
- * demonstration.py:18 assert) the item gets -2 and CRAFT_ETEACHER latches. */
+ * demonstration.py:18 assert) the item gets -2 and CRAFT_ETEACHER latches.
+ * slots[i] == -1 skips item i (action and path length -1, no error): the
+ * trainer's ref_actions[i] = -1 for a done env (trainers/imitation.py:50-51). */
 int craft_teacher(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* tasks,
                   int32_t* action_out, int32_t* path_len_out, void* stream);
 

@@ -8,7 +8,9 @@ DemonstrationTeacher BFS), struct-of-arrays in HBM, behind a C ABI
 from . import gamedef
 from .cookbook import Cookbook, Index, Task, TaskManager, compile_config, world_params
 from .sim import CraftSim, hash_actions, sample_scenarios, splitmix64, synthetic_specs
+from .dataset import Dataset
+from .rollout import ImitationRollout, RolloutInfo, do_rollout
 
 __all__ = ["gamedef", "Cookbook", "Index", "Task", "TaskManager", "compile_config",
            "world_params", "CraftSim", "hash_actions", "sample_scenarios", "splitmix64",
-           "synthetic_specs"]
+           "synthetic_specs", "Dataset", "ImitationRollout", "RolloutInfo", "do_rollout"]

@@ -211,6 +211,11 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   const int64_t slot = a.slots ? (int64_t)a.slots[i] : i;
+  if (slot == -1) {                    // skipped item: the trainer's ref_action for a done env
+    a.act_out[i] = -1;
+    if (a.len_out) a.len_out[i] = -1;
+    return;
+  }
   if (slot < 0 || slot >= v.n_envs) {
     latch_error(v.err, CRAFT_ERANGE, i);
     a.act_out[i] = -2;

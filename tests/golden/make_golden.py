@@ -462,7 +462,130 @@ def gen_teacher(w12_grids, n_states=400):
     print("teacher_12x12.npz", np.unique(np.asarray(acts), return_counts=True))
 
 
+def fake_policy_weights(F, seed=11):
+    """A deterministic integer 'student' for the rollout fixtures: action =
+    argmax(features @ Wt[t % 3] * 8 + bias), exact in fp32 and float64 alike."""
+    rng = np.random.RandomState(seed)
+    Wt = rng.randint(-3, 4, size=(3, F, 6)).astype(np.int8)
+    bias = np.asarray([0, 1, 2, 3, 4, -64], dtype=np.int32)
+    return Wt, bias
+
+
+def load_imitation_trainer():
+    """trainers/imitation.py alone (trainers/__init__ pulls in the language
+    trainers, which this fixture does not need)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_trainers_imitation",
+                                                  os.path.join(REF, "trainers", "imitation.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.ImitationTrainer
+
+
+class FakeStudent:
+    """students/imitation.py's protocol (init/act/receive) around fake_policy_weights."""
+
+    def __init__(self, Wt, bias):
+        self.Wt, self.bias = Wt.astype(np.int64), bias.astype(np.int64)
+
+    def init(self, tasks, states, is_eval):
+        self.t = 0
+        self.received = []
+
+    def act(self, states):
+        f = np.stack([s.features() for s in states]).astype(np.int64)
+        scores = f @ self.Wt[self.t % 3] * 8 + self.bias
+        self.t += 1
+        return [int(a) for a in scores.argmax(axis=1)]
+
+    def receive(self, ref_actions):
+        self.received.append(list(ref_actions))
+
+
+def gen_imitation(w12_grids):
+    """ImitationTrainer.do_rollout (trainers/imitation.py:18-101) run by the
+    reference with its DemonstrationTeacher and a deterministic fake student:
+    (a) the first 256 craft_medium dev instances, policy mix 0.5 and eval;
+    (b) 256 envs on 12x12 sampled worlds, policy mix 0.3."""
+    Trainer = load_imitation_trainer()
+    arrays = {}
+    for case in ["dev8", "w12"]:
+        if case == "dev8":
+            cfg, world = make_world()
+            data = json.load(open(os.path.join(REF, "data", "craft_medium_dev.json")))
+        else:
+            cfg, world = make_world(12, 3)
+        tm = TaskManager(cfg)
+        task_ids = {f"{t.goal_name}[{t.goal_arg}]": i for i, t in enumerate(tm.tasks)}
+        K = world.cookbook.n_kinds
+        W = world.WIDTH
+        teacher = teachers.load(cfg)
+        batch, spec = [], []
+        if case == "dev8":
+            pool = []
+            for item in data:
+                ids = onehot_to_ids(item["grid"]).reshape(-1)
+                pool.append(ids)
+                for ti in item["task_instances"]:
+                    for p in ti["init_pos"]:
+                        batch.append({"task": tm[ti["task"]], "grid": np.array(item["grid"]),
+                                      "init_pos": tuple(p)})
+                        spec.append([len(pool) - 1, p[0], p[1], 0, task_ids[ti["task"]]])
+            batch, spec = batch[:256], spec[:256]
+            mix = 0.5
+        else:
+            pool = list(w12_grids[:32])
+            rng = np.random.RandomState(21)
+            tasks = [i for i, t in enumerate(tm.tasks) if t.goal_name in ("get", "make")]
+            for e in range(256):
+                sc = e % len(pool)
+                g = pool[sc].reshape(W, W)
+                free = [(x, y) for x in range(1, W - 1) for y in range(1, W - 1) if g[x, y] == 0]
+                x, y = free[rng.randint(len(free))]
+                tk = tasks[rng.randint(len(tasks))]
+                batch.append({"task": list(tm.tasks)[tk],
+                              "grid": ids_to_onehot(g, K), "init_pos": (x, y)})
+                spec.append([sc, x, y, 0, tk])
+            mix = 0.3
+        Wt, bias = fake_policy_weights(world.n_features)
+        student = FakeStudent(Wt, bias)
+        cfg.random = np.random.RandomState(77)
+        trainer = Trainer(cfg)
+        trainer.policy_mix_rate = mix
+        for is_eval in [False, True]:
+            st = cfg.random.get_state()
+            bc = np.random.RandomState(0)
+            bc.set_state(st)
+            bc_mask = bc.binomial(1, mix, size=len(batch)) if not is_eval else np.zeros(len(batch), int)
+            info = trainer.do_rollout(batch, world, student, teacher, is_eval)
+            key = f"{case}_{'eval' if is_eval else 'train'}"
+            L = max(len(a) for a in info["action_seqs"])
+            A = np.full((len(batch), 40), -1, dtype=np.int8)
+            for i, a in enumerate(info["action_seqs"]):
+                A[i, :len(a)] = a
+            arrays[key + "_action_seqs"] = A
+            arrays[key + "_success"] = np.asarray(info["success"], dtype=np.int8)
+            arrays[key + "_distances"] = np.asarray(info["distances"], dtype=np.int16)
+            arrays[key + "_counts"] = np.asarray([info["num_interactions"], info["num_steps"]],
+                                                 dtype=np.int64)
+            arrays[key + "_bc"] = bc_mask.astype(np.uint8)
+            R = np.asarray(student.received, dtype=np.int8) if student.received else \
+                np.zeros((0, len(batch)), dtype=np.int8)
+            arrays[key + "_received"] = R
+            print("imitation", key, "ticks", len(student.received) or student.t, "max len", L,
+                  "success", int(np.sum(info["success"])), "counts", arrays[key + "_counts"])
+        arrays[case + "_pool"] = np.stack(pool).astype(np.uint8)
+        arrays[case + "_spec"] = np.asarray(spec, dtype=np.int32)
+        arrays[case + "_W"] = Wt
+        arrays[case + "_bias"] = bias
+    np.savez_compressed(os.path.join(OUT, "imitation_rollout.npz"), **arrays)
+    print("imitation_rollout.npz", os.path.getsize(os.path.join(OUT, "imitation_rollout.npz")))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["imitation"]:           # only the do_rollout fixture
+        gen_imitation(np.load(os.path.join(OUT, "scenarios_seed123.npz"))["w12_grids"])
+        sys.exit(0)
     cfg, world, tm = gen_cookbook()
     gen_devtest(tm)
     sc = gen_scenarios()
@@ -471,3 +594,4 @@ if __name__ == "__main__":
     gen_teacher(sc["w12_grids"])
     gen_rollout(sc["w12_grids"], 3, T=100, E=64, P=16, all_obs_ticks=None)
     gen_rollout(sc["w12_grids"], 5, T=60, E=48, P=16, all_obs_ticks=None)
+    gen_imitation(sc["w12_grids"])

@@ -1,0 +1,115 @@
+"""Batched do_rollout (psketch_amd.rollout) against the reference's
+ImitationTrainer.do_rollout (tests/golden/imitation_rollout.npz) and the oracle
+restatement (oracle/rollout_oracle.py) at larger sizes."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import make_tables
+
+pytestmark = pytest.mark.gpu
+
+
+def torch_policy(W, bias, device):
+    """fake_policy of make_golden.py on the device: exact (small integers in float64)."""
+    Wd = torch.as_tensor(np.asarray(W, dtype=np.float64), device=device)
+    bd = torch.as_tensor(np.asarray(bias, dtype=np.float64), device=device)
+
+    def act(obs, t):
+        return (obs.double() @ Wd[t % Wd.shape[0]] * 8 + bd).argmax(dim=1).to(torch.int32)
+    return act
+
+
+@pytest.mark.parametrize("case", ["dev8", "w12"])
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode):
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import do_rollout
+    fx = golden("imitation_rollout.npz")
+    world = {"dev8": "craft_medium", "w12": "craft_medium_12x12"}[case]
+    pool, spec = fx[f"{case}_pool"], fx[f"{case}_spec"]
+    key = f"{case}_{mode}"
+    sim = CraftSim(world, n_envs=len(spec), device=gpu.index, pool_capacity=len(pool))
+    sim.load_pool(pool)
+    received = []
+    info = do_rollout(sim, tuple(spec.T), torch_policy(fx[f"{case}_W"], fx[f"{case}_bias"], gpu),
+                      mode == "eval", behavior_clone=fx[key + "_bc"],
+                      receive=lambda r: received.append(r.cpu().numpy()))
+    ref = info.to_reference()
+    A = fx[key + "_action_seqs"]
+    assert ref["action_seqs"] == [[int(a) for a in row if a >= 0] for row in A]
+    assert ref["success"] == [bool(s) for s in fx[key + "_success"]]
+    assert ref["distances"] == fx[key + "_distances"].tolist()
+    assert [ref["num_interactions"], ref["num_steps"]] == fx[key + "_counts"].tolist()
+    R = fx[key + "_received"]
+    assert np.array_equal(np.asarray(received, dtype=np.int8).reshape(R.shape), R)
+
+
+@pytest.mark.parametrize("world,n", [("craft_medium_12x12", 2048), ("craft_medium_12x12_w5", 512)])
+def test_do_rollout_vs_oracle(golden, gpu, oracle_mod, world, n):
+    """Random policy-mix rollouts on sampled 12x12 worlds, with every observation the
+    student saw (keep_obs) checked against the oracle's features()."""
+    from oracle import rollout_oracle
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import do_rollout
+    from psketch_amd.sim import synthetic_specs
+    sc = golden("scenarios_seed123.npz")
+    pool = sc["w12_grids"]
+    _, _, tm, cfg = make_tables(world)
+    tasks = [t.id for t in tm.dataset_tasks()]
+    spec = np.stack(synthetic_specs(pool, 12, 12, n, seed=5, task_ids=tasks), axis=1)
+    spec[:, 3] = np.arange(n) % 4                   # non-default initial directions too
+    rng = np.random.RandomState(9)
+    bc = rng.binomial(1, 0.5, size=n)
+    W = rng.randint(-3, 4, size=(3, cfg.n_features, 6))
+    bias = np.asarray([0, 1, 2, 3, 4, -40])
+    seen = []
+
+    def act_cpu(obs, t):
+        seen.append(obs.copy())
+        return rollout_oracle.fake_policy(W, bias)(obs, t)
+
+    expect = rollout_oracle.do_rollout(oracle_mod.Oracle(cfg, pool), spec, act_cpu, False,
+                                       bc_mask=bc)
+    sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    sim.load_pool(pool)
+    received = []
+    info = do_rollout(sim, tuple(spec.T), torch_policy(W, bias, gpu), False, behavior_clone=bc,
+                      receive=lambda r: received.append(r.cpu().numpy()), keep_obs=True)
+    got = info.to_reference()
+    for k in ["action_seqs", "success", "distances", "num_interactions", "num_steps"]:
+        assert got[k] == expect[k], k
+    assert np.array_equal(np.asarray(received), np.asarray(expect["received"]))
+    assert info.ticks == len(seen)
+    obs = info.obs.cpu().numpy()
+    for t in range(info.ticks):
+        assert np.array_equal(obs[t], seen[t]), t
+
+
+def test_imitation_rollout_replays_dataset(golden, gpu):
+    """Dataset batches (data/dataset.py) through ImitationRollout in eval mode, the
+    student replaying the reference's demonstrations: every episode succeeds, the
+    recorded sequences are the demonstrations, get-task distances are 0."""
+    from psketch_amd.dataset import Dataset
+    from psketch_amd.rollout import ImitationRollout
+    from tests.test_host import devtest_as_json
+    fx = golden("devtest.npz")
+    _, cb, tm, _ = make_tables("craft_medium")
+    ds = Dataset(devtest_as_json(fx, "dev", tm, cb.n_kinds), "dev", tm,
+                 random=np.random.RandomState(1), batch_size=500)
+    runner = ImitationRollout("craft_medium", ds.pool_array(), device=gpu.index)
+    total = 0
+    for batch in ds.iterate_batches():
+        A = np.full((40, len(batch)), 5, dtype=np.int32)
+        for i, it in enumerate(batch):
+            A[:len(it["ref_actions"]), i] = it["ref_actions"]
+        Ad = torch.as_tensor(A, device=gpu)
+        info = runner.do_rollout(batch, lambda obs, t: Ad[t], is_eval=True)
+        ref = info.to_reference()
+        assert ref["action_seqs"] == [list(it["ref_actions"]) for it in batch]
+        assert all(ref["success"])
+        assert ref["distances"] == [0] * sum(it["task"].goal_name == "get" for it in batch)
+        total += len(batch)
+    assert total == len(ds)
+    # last batch has a different size: a second simulator was created for it
+    assert len(runner._sims) == 2

@@ -135,3 +135,75 @@ def test_hash_actions_uniform():
     a = hash_actions(0, np.arange(60000), 5)
     counts = np.bincount(a, minlength=6)
     assert counts.min() > 9500 and counts.max() < 10500
+
+
+def devtest_as_json(fx, split, tm, K):
+    """Rebuilds the reference's split-file structure (data/craft_medium_{split}.json)
+    from the compact devtest.npz fixture: same worlds, tasks, positions, ids."""
+    names = [f"{t.goal_name}[{t.goal_arg}]" for t in tm.tasks]
+    grids = fx[f"{split}_grids"]
+    world, task, pos = fx[f"{split}_world"], fx[f"{split}_task"], fx[f"{split}_pos"]
+    acts, ids = fx[f"{split}_actions"], fx[f"{split}_ids"]
+    out = []
+    W = int(round(np.sqrt(grids.shape[1])))
+    for wi in range(len(grids)):
+        g = grids[wi].reshape(W, W)
+        onehot = (g[..., None] == np.arange(K)[None, None, :]) & (g[..., None] > 0)
+        item = {"grid": onehot.astype(float).tolist(), "task_instances": []}
+        sel = np.nonzero(world == wi)[0]
+        for tk in dict.fromkeys(task[sel].tolist()):
+            rows = sel[task[sel] == tk]
+            item["task_instances"].append({
+                "task": names[tk], "init_pos": pos[rows].tolist(),
+                "ids": [f"{split}_{i}" for i in ids[rows]],
+                "ref_actions": [[int(a) for a in acts[r] if a >= 0] for r in rows]})
+        out.append(item)
+    return out
+
+
+def test_dataset_flatten_and_batches(golden):
+    """psketch_amd.dataset.Dataset == data/dataset.py:47-86: flattening order,
+    one-hot grid -> scenario pool, next_batch's shuffling through config.random."""
+    from psketch_amd.dataset import Dataset
+    fx = golden("devtest.npz")
+    _, cb, tm, _ = make_tables("craft_medium")
+    data = devtest_as_json(fx, "dev", tm, cb.n_kinds)
+    ds = Dataset(data, "dev", tm, random=np.random.RandomState(3), batch_size=32)
+    n = len(fx["dev_task"])
+    assert len(ds) == n
+    spec = np.stack(Dataset.specs(list(ds)), axis=1)
+    # the fixture's own order is the flattening order of the reference
+    first_seen = {w: i for i, w in enumerate(dict.fromkeys(fx["dev_world"].tolist()))}
+    assert np.array_equal(spec[:, 0], [first_seen[w] for w in fx["dev_world"]])
+    assert np.array_equal(spec[:, 1:3], fx["dev_pos"])
+    assert np.array_equal(spec[:, 4], fx["dev_task"])
+    assert [it["id"] for it in ds] == [f"dev_{i}" for i in fx["dev_ids"]]
+    assert np.array_equal(ds.pool_array()[spec[:, 0]], fx["dev_grids"][fx["dev_world"]])
+    # next_batch: the reference shuffles list(range(n)) with config.random on every pass
+    rs = np.random.RandomState(3)
+    for _ in range(2):
+        order = list(range(n))
+        rs.shuffle(order)
+        got = [it["id"] for b in ds.iterate_batches() for it in b]
+        assert got == [ds[i]["id"] for i in order]
+    with pytest.raises(AssertionError):
+        bad = devtest_as_json(fx, "dev", tm, cb.n_kinds)[:1]
+        bad[0]["grid"][1][1][3] = 1.0
+        bad[0]["grid"][1][1][4] = 1.0
+        Dataset(bad, "dev", tm)
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/data"), reason="reference split files absent")
+def test_dataset_reads_reference_split_files(golden):
+    """The committed split JSON files themselves (build container only)."""
+    from psketch_amd.dataset import Dataset
+    fx = golden("devtest.npz")
+    _, _, tm, _ = make_tables("craft_medium")
+    for split in ["dev", "test"]:
+        ds = Dataset(f"/root/reference/data/craft_medium_{split}.json", split, tm)
+        spec = np.stack(Dataset.specs(list(ds)), axis=1)
+        assert np.array_equal(spec[:, 1:3], fx[f"{split}_pos"])
+        assert np.array_equal(spec[:, 4], fx[f"{split}_task"])
+        assert np.array_equal(ds.pool_array()[spec[:, 0]], fx[f"{split}_grids"][fx[f"{split}_world"]])
+        L = fx[f"{split}_actions"]
+        assert all(tuple(int(a) for a in L[i] if a >= 0) == it["ref_actions"] for i, it in enumerate(ds))

@@ -178,3 +178,32 @@ def test_hash_action_matches(oracle_mod):
     for tick in (0, 1, 99, 12345):
         ref = [oracle_mod.hash_action(42, int(g), tick) for g in gids]
         assert hash_actions(42, gids, tick).tolist() == ref
+
+
+def _imitation_case(golden, case):
+    fx = golden("imitation_rollout.npz")
+    world = {"dev8": "craft_medium", "w12": "craft_medium_12x12"}[case]
+    return fx, world
+
+
+@pytest.mark.parametrize("case", ["dev8", "w12"])
+@pytest.mark.parametrize("mode", ["train", "eval"])
+def test_oracle_do_rollout_matches_reference(golden, oracle_mod, case, mode):
+    """oracle/rollout_oracle.do_rollout == the reference's ImitationTrainer.do_rollout
+    (trainers/imitation.py:18-101) with its DemonstrationTeacher and a fixed student."""
+    from oracle import rollout_oracle
+    fx, world = _imitation_case(golden, case)
+    _, _, _, cfg = make_tables(world)
+    orc = oracle_mod.Oracle(cfg, fx[f"{case}_pool"])
+    key = f"{case}_{mode}"
+    act = rollout_oracle.fake_policy(fx[f"{case}_W"], fx[f"{case}_bias"])
+    info = rollout_oracle.do_rollout(orc, fx[f"{case}_spec"], act, mode == "eval",
+                                     bc_mask=fx[key + "_bc"])
+    A = fx[key + "_action_seqs"]
+    for i, seq in enumerate(info["action_seqs"]):
+        assert seq == [int(a) for a in A[i] if a >= 0], i
+    assert np.array_equal(np.asarray(info["success"], dtype=np.int8), fx[key + "_success"])
+    assert info["distances"] == fx[key + "_distances"].tolist()
+    assert [info["num_interactions"], info["num_steps"]] == fx[key + "_counts"].tolist()
+    R = fx[key + "_received"]
+    assert np.array_equal(np.asarray(info["received"], dtype=np.int8).reshape(R.shape), R)
