@@ -148,6 +148,19 @@ int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capaci
 int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu,
                    int32_t obs_store);
 
+/* Element type of every observation buffer this handle writes (craft_reset,
+ * craft_step, craft_step_ex, craft_observe).  The features are small
+ * non-negative integers (one-hots, block maxima, inventory counts < 256), so
+ * all three formats hold exactly the reference's values; bf16 and u8 cut the
+ * observation stream (the kernel's dominant HBM traffic) by 2x and 4x for a
+ * student that consumes them directly.  Default CRAFT_OBS_F32. */
+typedef enum {
+  CRAFT_OBS_F32 = 0,
+  CRAFT_OBS_BF16 = 1,
+  CRAFT_OBS_U8 = 2
+} craft_obs_format_t;
+int craft_sim_set_obs_format(craft_sim_t* sim, int32_t format);
+
 /* Synchronises `stream` and returns the first kernel-side error latched since
  * the last call (then clears it); *env_out receives the offending slot. */
 int craft_sim_check(craft_sim_t* sim, int64_t* env_out, void* stream);
@@ -166,11 +179,11 @@ int craft_pool_load(craft_sim_t* sim, const uint8_t* grids, int32_t first, int32
 /* CraftScenario.init (craft.py:262-273) for every slot: inventory zeroed,
  * grid = pool[scenario], pos/dir given, timer = max_timesteps.  The spec is
  * kept so that an auto-reset returns the slot to the same initial state.
- * Device arrays of n_envs int32 each; `obs` (n_envs x n_features fp32) may be
+ * Device arrays of n_envs int32 each; `obs` (n_envs x n_features, obs format) may be
  * NULL, else receives features() of the initial states. */
 int craft_reset(craft_sim_t* sim, const int32_t* scenario, const int32_t* pos_x,
                 const int32_t* pos_y, const int32_t* dir, const int32_t* task,
-                float* obs, void* stream);
+                void* obs, void* stream);
 
 #define CRAFT_STEP_AUTORESET 1u   /* done slots restart from their spec next tick */
 
@@ -184,15 +197,42 @@ int craft_reset(craft_sim_t* sim, const int32_t* scenario, const int32_t* pos_x,
  *   !done -> state = step(state, a)            (craft.py:332-424)
  * `actions` (device int32[n_envs]) may be NULL: actions are then drawn in the
  * kernel as splitmix64(action_seed ^ (gid << 20) ^ tick) >> 32 mod 6.
- * Outputs (device, each may be NULL): obs fp32[n_envs][n_features];
+ * Outputs (device, each may be NULL): obs [n_envs][n_features] (obs format);
  * reward fp32 (1 on a tick that ends an episode with satisfies() true, else 0 —
  * step() itself always returns 0, craft.py:338); done uint8; success int8
  * (-1 not terminal, else satisfies()).  Episode statistics accumulate inside
  * the handle (per-workgroup partial sums, no atomics); read them with
  * craft_stats. */
 int craft_step(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed, int64_t tick,
-               uint32_t flags, float* obs, float* reward, uint8_t* done, int8_t* success,
+               uint32_t flags, void* obs, float* reward, uint8_t* done, int8_t* success,
                void* stream);
+
+/* craft_step with the rest of a do_rollout tick fused in (trainers/imitation.py:43-73):
+ *   a = behavior_clone[i] ? ref_actions[i] : actions[i]     (imitation.py:56-57)
+ *   action_record[i] = a, or -1 for a slot already done     (action_seqs, :59-61)
+ *   *any_live = 1 if some slot is still running after this tick (all(done), :42)
+ * then the craft_step tick.  ref_actions is craft_teacher's output for the same
+ * slots (a done slot's label is -1 and is never used).  Every pointer may be
+ * NULL: actions NULL = the hashed draw; ref_actions/behavior_clone NULL = no
+ * cloning.  any_live is a device int32 the kernel only ever sets to 1 (plain
+ * stores, no atomics: point it at element t of a zeroed per-tick array).  The
+ * rollout counters come from craft_stats: num_interactions (:54) = env-steps,
+ * num_steps (:71) = env-steps - episodes ended.  obs has the handle's obs format. */
+typedef struct {
+  const int32_t* actions;          /* int32[n_envs] student actions */
+  const int32_t* ref_actions;      /* int32[n_envs] teacher labels */
+  const uint8_t* behavior_clone;   /* uint8[n_envs] 0/1 */
+  uint64_t action_seed;
+  int64_t tick;
+  uint32_t flags;                  /* CRAFT_STEP_AUTORESET */
+  void* obs;                       /* [n_envs][n_features] in the obs format */
+  float* reward;
+  uint8_t* done;
+  int8_t* success;
+  int32_t* action_record;          /* int32[n_envs] */
+  int32_t* any_live;               /* int32 scalar flag */
+} craft_step_args_t;
+int craft_step_ex(craft_sim_t* sim, const craft_step_args_t* args, void* stream);
 
 /* Sums the episode statistics accumulated by craft_step into stats_out
  * (device int64[3] = {successes, episodes ended, env-steps}) — the scalar
@@ -210,10 +250,10 @@ int craft_transition(craft_sim_t* sim, const int32_t* src, const int32_t* dst,
                      const int32_t* actions, int64_t n, void* stream);
 
 /* CraftState.features() (craft.py:296-330) and satisfies() (craft.py:285-294)
- * for n slots (NULL = identity).  obs: fp32[n][n_features] or NULL; sat: int8[n]
+ * for n slots (NULL = identity).  obs: [n][n_features] (obs format) or NULL; sat: int8[n]
  * (-1 = None, 0/1) for task tasks[i] (NULL = the slot's own task) or NULL. */
 int craft_observe(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* tasks,
-                  float* obs, int8_t* sat, void* stream);
+                  void* obs, int8_t* sat, void* stream);
 
 /* DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for n slots:
  * find_incomplete_subtask over the hint tree then the BFS of
@@ -223,7 +263,8 @@ int craft_observe(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32
  * (the trainer's `distances`, trainers/imitation.py:79-91), -1 if no target.
  * Where the reference raises (base.py:24 assert, base.py:31 len(None),
  * demonstration.py:18 assert) the item gets -2 and CRAFT_ETEACHER latches.
- * slots[i] == -1 skips item i (action and path length -1, no error): the
+ * slots[i] == -1 skips item i, and a frozen slot (an episode craft_step ended
+ * without auto-reset) yields action -1 (path length -1, no error): the
  * trainer's ref_actions[i] = -1 for a done env (trainers/imitation.py:50-51). */
 int craft_teacher(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* tasks,
                   int32_t* action_out, int32_t* path_len_out, void* stream);

@@ -71,6 +71,25 @@ class craft_config_t(ctypes.Structure):
     ]
 
 
+class craft_step_args_t(ctypes.Structure):
+    _fields_ = [
+        ("actions", ctypes.c_void_p),
+        ("ref_actions", ctypes.c_void_p),
+        ("behavior_clone", ctypes.c_void_p),
+        ("action_seed", ctypes.c_uint64),
+        ("tick", ctypes.c_int64),
+        ("flags", ctypes.c_uint32),
+        ("obs", ctypes.c_void_p),
+        ("reward", ctypes.c_void_p),
+        ("done", ctypes.c_void_p),
+        ("success", ctypes.c_void_p),
+        ("action_record", ctypes.c_void_p),
+        ("any_live", ctypes.c_void_p),
+    ]
+
+
+OBS_F32, OBS_BF16, OBS_U8 = 0, 1, 2
+
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
@@ -88,9 +107,11 @@ SIGNATURES = {
                               ctypes.POINTER(_i32)]),
     "craft_sim_check": (_i32, [_vp, ctypes.POINTER(_i64), _vp]),
     "craft_sim_tune": (_i32, [_vp, _i32, _i32, _i32]),
+    "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_pool_load": (_i32, [_vp, _vp, _i32, _i32]),
     "craft_reset": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "craft_step": (_i32, [_vp, _vp, _u64, _i64, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "craft_step_ex": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp]),
     "craft_stats": (_i32, [_vp, _vp, _i32, _vp]),
     "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
     "craft_observe": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),

@@ -43,6 +43,7 @@ struct SimView {
   int32_t W, H, K, F, C, CS, GS, maxT;
   int32_t bridge, axe;
   int32_t obs_policy;         // observation stores: 0 write-back, 1 nontemporal, 2 write-through (sc1)
+  int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   const uint8_t* rc;          // [CRAFT_MAX_RECIPES][kRecipeBytes] compact recipes
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
@@ -81,10 +82,14 @@ struct TileArgs {
   int64_t tick;
   int64_t n;
   uint32_t flags;
-  float* obs;
+  void* obs;
   float* reward;
   uint8_t* done;
   int8_t* sat;
+  const int32_t* ref;      // MODE_TICK rollout fusion (craft_step_ex)
+  const uint8_t* bc;
+  int32_t* rec;
+  int32_t* any_live;
 };
 
 struct Agent {

@@ -36,9 +36,21 @@ __global__ void get_state_kernel(SimView v, const int32_t* slots, int64_t n, int
   if (grid_out) {
     const uint32_t* m = reinterpret_cast<const uint32_t*>(v.mask + 2 * slot);
     const bool ok = s.scen < v.pool_count;
-    for (int c = 0; c < v.C; ++c) {
-      const int k = ok ? v.pool[(size_t)s.scen * v.CS + c] : 0;
-      grid_out[i * v.C + c] = ((m[c >> 5] >> (c & 31)) & 1u) ? 0 : (uint8_t)k;
+    if ((v.C & 3) == 0) {               // whole dwords: 4 cells per load and per store
+      const uint32_t* row = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
+      uint32_t* out = reinterpret_cast<uint32_t*>(grid_out + i * v.C);
+      for (int q = 0; q < (v.C >> 2); ++q) {
+        uint32_t w = ok ? row[q] : 0u;
+        const uint32_t cleared = (m[q >> 3] >> ((q & 7) * 4)) & 0xfu;   // cells 4q..4q+3
+        for (int b = 0; b < 4; ++b)
+          if ((cleared >> b) & 1u) w &= ~(0xffu << (8 * b));
+        out[q] = w;
+      }
+    } else {
+      for (int c = 0; c < v.C; ++c) {
+        const int k = ok ? v.pool[(size_t)s.scen * v.CS + c] : 0;
+        grid_out[i * v.C + c] = ((m[c >> 5] >> (c & 31)) & 1u) ? 0 : (uint8_t)k;
+      }
     }
   }
   if (spec_out) {
@@ -318,6 +330,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.maxT = cfg->max_timesteps;
   v.bridge = cfg->bridge_kind;
   v.obs_policy = 1;   // nontemporal observation stores (fastest in tools/sweep_tiles.py)
+  v.obs_fmt = CRAFT_OBS_F32;
   v.axe = cfg->axe_kind;
   v.kc_lo = v.kc_hi = 0;
   for (int k = 0; k < CRAFT_MAX_KINDS; ++k) {
@@ -342,6 +355,14 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
   s->tile = tile_envs;
   s->resident_cap = max_resident_per_cu;
   s->view.obs_policy = obs_store;
+  return CRAFT_OK;
+}
+
+int craft_sim_set_obs_format(craft_sim_t* s, int32_t format) {
+  if (!s) return CRAFT_EINVAL;
+  if (format != CRAFT_OBS_F32 && format != CRAFT_OBS_BF16 && format != CRAFT_OBS_U8)
+    return fail(s, CRAFT_EINVAL, "craft_sim_set_obs_format: format must be 0 (fp32), 1 (bf16) or 2 (u8)");
+  s->view.obs_fmt = format;
   return CRAFT_OK;
 }
 
@@ -415,7 +436,7 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
 }
 
 int craft_reset(craft_sim_t* s, const int32_t* scenario, const int32_t* pos_x, const int32_t* pos_y,
-                const int32_t* dir, const int32_t* task, float* obs, void* stream) {
+                const int32_t* dir, const int32_t* task, void* obs, void* stream) {
   if (!s || !scenario || !pos_x || !pos_y || !dir || !task) return fail(s, CRAFT_EINVAL, "craft_reset: null input");
   if (obs && !aligned16(obs)) return fail(s, CRAFT_EINVAL, "craft_reset: obs must be 16-byte aligned");
   TileArgs a{};
@@ -429,19 +450,38 @@ int craft_reset(craft_sim_t* s, const int32_t* scenario, const int32_t* pos_x, c
 }
 
 int craft_step(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, int64_t tick, uint32_t flags,
-               float* obs, float* reward, uint8_t* done, int8_t* success, void* stream) {
-  if (!s) return CRAFT_EINVAL;
-  if (obs && !aligned16(obs)) return fail(s, CRAFT_EINVAL, "craft_step: obs must be 16-byte aligned");
+               void* obs, float* reward, uint8_t* done, int8_t* success, void* stream) {
+  craft_step_args_t x{};
+  x.actions = actions;
+  x.action_seed = action_seed;
+  x.tick = tick;
+  x.flags = flags;
+  x.obs = obs;
+  x.reward = reward;
+  x.done = done;
+  x.success = success;
+  return craft_step_ex(s, &x, stream);
+}
+
+int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
+  if (!s || !x) return CRAFT_EINVAL;
+  if (x->obs && !aligned16(x->obs)) return fail(s, CRAFT_EINVAL, "craft_step: obs must be 16-byte aligned");
+  if (x->behavior_clone && !x->ref_actions)
+    return fail(s, CRAFT_EINVAL, "craft_step_ex: behavior_clone needs ref_actions");
   TileArgs a{};
-  a.actions = actions;
-  a.seed = action_seed;
-  a.tick = tick;
-  a.flags = flags;
+  a.actions = x->actions;
+  a.seed = x->action_seed;
+  a.tick = x->tick;
+  a.flags = x->flags;
   a.n = s->n_envs;
-  a.obs = obs;
-  a.reward = reward;
-  a.done = done;
-  a.sat = success;
+  a.obs = x->obs;
+  a.reward = x->reward;
+  a.done = x->done;
+  a.sat = x->success;
+  a.ref = x->ref_actions;
+  a.bc = x->behavior_clone;
+  a.rec = x->action_record;
+  a.any_live = x->any_live;
   return launch(s, craft::MODE_TICK, a, stream, "craft_step launch");
 }
 
@@ -466,7 +506,7 @@ int craft_transition(craft_sim_t* s, const int32_t* src, const int32_t* dst, con
   return launch(s, craft::MODE_TRANSITION, a, stream, "craft_transition launch");
 }
 
-int craft_observe(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t* tasks, float* obs,
+int craft_observe(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t* tasks, void* obs,
                   int8_t* sat, void* stream) {
   if (!s || n < 0) return fail(s, CRAFT_EINVAL, "craft_observe: bad argument");
   if (!slots && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_observe: n > n_envs");

@@ -223,6 +223,11 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
     return;
   }
   const Agent s = unpack_state(v.state[slot]);
+  if (s.frozen) {                      // done env: its label is -1 (imitation.py:50-51)
+    a.act_out[i] = -1;
+    if (a.len_out) a.len_out[i] = -1;
+    return;
+  }
   const int task = a.tasks ? a.tasks[i] : s.task;
   if (task < 0 || task >= v.n_tasks || s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 ||
       s.scen >= v.pool_count) {

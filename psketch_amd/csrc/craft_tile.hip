@@ -11,8 +11,9 @@
 //   D  all threads scatter the observation's non-zero bytes (local-window
 //      one-hots, block-max-pooled one-hots, inventory counts, dir one-hot) into
 //      the tile's u8 rows [TILE][F] in LDS.
-//   E  all threads stream the rows to HBM as fp32: flat index s, one ds_read_b32
-//      of 4 feature bytes, 4 v_cvt_f32_ubyte, one contiguous 16-byte store.
+//   E  all threads stream the rows to HBM: flat index s, one LDS read, one
+//      contiguous 16-byte store (fp32: ds_read_b32 of 4 feature bytes and 4
+//      v_cvt_f32_ubyte; bf16: 8 bytes; u8: 16 bytes as they are).
 // The kernel is bound by E's HBM writes (F*4 = 1616 B per env at w=3).  See
 // DESIGN.md for the roofline and the phase timings that shaped this layout.
 #include "craft_device.h"
@@ -51,6 +52,63 @@ __device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int
   const int xc = min(max(cx, 0), W - 1), yc = min(max(cy, 0), H - 1);
   const int k = g[xc * H + yc];
   return ok ? (1u << k) : 0u;
+}
+
+// 16 bytes of output from the tile's u8 feature rows: 4 fp32 (v_cvt_f32_ubyte),
+// 8 bf16 (the high half of the exact fp32 value of a byte) or 16 u8.
+template <int FMT>
+__device__ __forceinline__ obs_vec pack16(const uint8_t* s_obs, int sidx) {
+  if (FMT == CRAFT_OBS_F32) {
+    const uint32_t w = reinterpret_cast<const uint32_t*>(s_obs)[sidx];
+    return obs_vec{__float_as_uint((float)(w & 0xff)), __float_as_uint((float)((w >> 8) & 0xff)),
+                   __float_as_uint((float)((w >> 16) & 0xff)), __float_as_uint((float)(w >> 24))};
+  } else if (FMT == CRAFT_OBS_BF16) {
+    const uint2 w = reinterpret_cast<const uint2*>(s_obs)[sidx];
+    auto bf = [](uint32_t b) { return __float_as_uint((float)b) >> 16; };
+    auto two = [&](uint32_t x) { return bf(x & 0xff) | (bf((x >> 8) & 0xff) << 16); };
+    return obs_vec{two(w.x), two(w.x >> 16), two(w.y), two(w.y >> 16)};
+  } else {
+    const uint4 w = reinterpret_cast<const uint4*>(s_obs)[sidx];
+    return obs_vec{w.x, w.y, w.z, w.w};
+  }
+}
+
+// Phase E: the tile's rows are contiguous in the output, so the whole tile is one
+// flat stream of 16-byte buffer stores (32-bit offsets off one wave-uniform
+// descriptor); the cache policy is a tuning knob (craft_sim_tune).
+template <int FMT>
+__device__ __forceinline__ void stream_obs(const uint8_t* s_obs, void* obs, int64_t env0, int F, int nE,
+                                           int policy, int tid) {
+  constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
+  constexpr int PER = 16 / ESZ;                // values per 16-byte store
+  const int total = nE * F;
+  const int nv = total / PER;
+  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
+  constexpr int U = 4;                         // independent 16-byte stores in flight per lane
+  for (int base = tid; base < nv; base += U * kThreads) {
+    obs_vec o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sidx = base + u * kThreads;
+      if (sidx < nv) o[u] = pack16<FMT>(s_obs, sidx);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sidx = base + u * kThreads;
+      if (sidx < nv) {
+        if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 2);         // nt
+        else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 16);   // sc1
+        else __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 0);
+      }
+    }
+  }
+  for (int f = nv * PER + tid; f < total; f += kThreads) {   // the last few values of the tile
+    const uint32_t b = s_obs[f];
+    if (FMT == CRAFT_OBS_F32) reinterpret_cast<float*>(tile_out)[f] = (float)b;
+    else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint16_t*>(tile_out)[f] = (uint16_t)(__float_as_uint((float)b) >> 16);
+    else tile_out[f] = (uint8_t)b;
+  }
 }
 
 template <int WIN, int MODE, int TILE>
@@ -114,6 +172,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
             const uint64_t gid = (uint64_t)(v.env_base + slot);
             act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)a.tick) >> 32) % 6u);
           }
+          if (a.bc && a.bc[slot]) act = a.ref[slot];    // behaviour cloning, imitation.py:56-57
         } else if (MODE == MODE_TRANSITION) {
           act = a.actions[env0 + tid];
         }
@@ -244,6 +303,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
         if (a.done) a.done[i] = (uint8_t)d;
         if (a.sat) a.sat[i] = (int8_t)succ;
         if (a.reward) a.reward[i] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+        if (a.rec) a.rec[i] = counted ? act : -1;        // action_seqs, imitation.py:59-61
       }
     }
     s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
@@ -252,11 +312,13 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
       const uint64_t bs = __ballot(live && counted && d && succ == 1);
       const uint64_t be = __ballot(live && counted && d);
       const uint64_t bt = __ballot(live && counted);
+      const uint64_t bl = __ballot(live && counted && !d);
       if (tid == 0) {   // no-return atomics: the wave does not wait for them
         unsigned long long* r = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
         atomicAdd(r + 0, (unsigned long long)__popcll(bs));
         atomicAdd(r + 1, (unsigned long long)__popcll(be));
         atomicAdd(r + 2, (unsigned long long)__popcll(bt));
+        if (a.any_live && bl) *a.any_live = 1;          // idempotent plain store
       }
     }
   } else if (want_obs) {
@@ -327,40 +389,11 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   __syncthreads();
   STAMP(5);
 
-  // ---- E: stream the tile's rows to HBM as fp32 ------------------------------------------------
-  {
-    const int total = nE * F;                  // floats in this tile (rows are contiguous)
-    const int n4 = total >> 2;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(s_obs);
-    float* tile_out = a.obs + env0 * (int64_t)F;
-    // Buffer stores: 32-bit offsets off one wave-uniform descriptor; the cache
-    // policy of the observation stream is a tuning knob (craft_sim_tune).
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * 4, 0x00020000);
-    constexpr int U = 4;                       // independent 16-byte stores in flight per lane
-    for (int base = tid; base < n4; base += U * kThreads) {
-      uint32_t w[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int sidx = base + u * kThreads;
-        w[u] = sidx < n4 ? src[sidx] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int sidx = base + u * kThreads;
-        if (sidx < n4) {
-          const float4 f = make_float4((float)(w[u] & 0xff), (float)((w[u] >> 8) & 0xff),   // v_cvt_f32_ubyte0..3
-                                       (float)((w[u] >> 16) & 0xff), (float)(w[u] >> 24));
-          const obs_vec o = {__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
-          if (v.obs_policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, sidx * 16, 0, 2);         // nt
-          else if (v.obs_policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, sidx * 16, 0, 16);   // sc1
-          else __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, sidx * 16, 0, 0);
-        }
-      }
-    }
-    if (tid < (total & 3)) {                   // F % 4 != 0: the last few floats
-      const int f = (n4 << 2) + tid;
-      a.obs[env0 * (int64_t)F + f] = (float)s_obs[f];
-    }
+  // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
+  switch (v.obs_fmt) {
+    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    default: stream_obs<CRAFT_OBS_F32>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
   }
   STAMP_END();
 }

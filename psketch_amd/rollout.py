@@ -6,13 +6,13 @@ live env, the behaviour-cloning substitution, the timer/STOP protocol, step.
 Here the whole batch lives in CraftSim slots and every per-env part of a tick is
 a kernel on the current stream:
 
-  teacher(slots = live ? slot : -1)   ref_actions, -1 for done envs  (imitation.py:47-55)
-  where(bc, ref, student)             behaviour cloning              (imitation.py:56-57)
-  record                              action_seqs                    (imitation.py:59-61)
-  craft_step (no auto-reset)          timer/STOP/satisfies/step + features  (imitation.py:63-73)
+  craft_teacher           ref_actions, -1 for done (frozen) envs      (imitation.py:47-55)
+  craft_step_ex           bc ? ref : student (imitation.py:56-57), action_seqs row
+                          (:59-61), timer/STOP/satisfies/step + features (:63-73),
+                          and an any-env-still-running flag (:42)
 
 The student sees the features as a device tensor and returns device actions;
-nothing crosses PCIe inside the loop except the all(done) test (one scalar per
+nothing crosses PCIe inside the loop except the all(done) test (one int32 per
 tick, imitation.py:42).  After the loop, `distances` (imitation.py:79-91) come
 from the same teacher kernel: failed get-tasks are reset to their initial grid
 at their final position and find_closest_resources' length is read back.
@@ -35,7 +35,7 @@ class RolloutInfo:
     action_seqs int32 [T, n] (-1 after an env's last action), n_actions int32 [n],
     success int8 [n], distances int32 [n] (-1 where the task is not a get task),
     is_get bool [n], num_interactions / num_steps ints, ticks, and obs
-    (fp32 [T+1, n, F], every observation the student saw) when kept."""
+    ([T+1, n, F], every observation the student saw) when kept."""
 
     def __init__(self, **kw):
         self.__dict__.update(kw)
@@ -56,43 +56,67 @@ class RolloutInfo:
         }
 
 
-def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_obs=False):
+def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_obs=False,
+               timing=None):
     """One rollout of sim.n_envs episodes.
 
     spec: (scenario, x, y, dir, task), each n_envs ints (device or host).
     act(obs, t) -> int device tensor [n]: the student (students/imitation.py act);
-      obs is fp32 [n, F] on the device and is overwritten by the next step
-      unless keep_obs.
+      obs is [n, F] on the device in the simulator's obs format (fp32 unless
+      sim.set_obs_format) and is overwritten by the next step unless keep_obs.
     behavior_clone: [n] 0/1 (config.random.binomial(1, policy_mix_rate, n),
       imitation.py:39-41); ignored when is_eval.
     receive(ref_actions) is called once per tick when not is_eval
       (student.receive, imitation.py:75-77) with the int32 device tensor.
+    timing: optional dict; receives host wall seconds of the setup, the tick
+      loop and the distances/summary phases (each ends at a device sync).
     """
+    import time
+    t_start = time.perf_counter()
     n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
     if T <= 0:
         raise ValueError("max_timesteps must be positive")
     spec = [sim._i32(a, n) for a in spec]
     task = spec[4]
     slot_ids = torch.arange(n, dtype=torch.int32, device=dev)
-    obs_hist = (torch.empty((T + 1, n, sim.n_features), dtype=torch.float32, device=dev)
+    obs_hist = (torch.empty((T + 1, n, sim.n_features), dtype=sim.obs_dtype, device=dev)
                 if keep_obs else None)
     obs = obs_hist[0] if keep_obs else sim.empty_obs()
     sim.reset(*spec, obs=obs)
-    done = torch.zeros(n, dtype=torch.uint8, device=dev)
-    done_b = torch.zeros(n, dtype=torch.bool, device=dev)
     success = torch.zeros(n, dtype=torch.int8, device=dev)
     seqs = torch.full((T, n), -1, dtype=torch.int32, device=dev)
+    live = torch.zeros(T, dtype=torch.int32, device=dev)     # 1: some env still running after tick t
     ref = torch.empty(n, dtype=torch.int32, device=dev)
-    interactions = torch.zeros((), dtype=torch.int64, device=dev)
-    steps = torch.zeros((), dtype=torch.int64, device=dev)
     bc = None
     if not is_eval:
         if behavior_clone is None:
             raise ValueError("behavior_clone is required when not is_eval")
         bc = torch.as_tensor(np.asarray(behavior_clone) if not torch.is_tensor(behavior_clone)
-                             else behavior_clone, device=dev).to(torch.bool)
+                             else behavior_clone, device=dev)
         if bc.numel() != n:
             raise ValueError(f"behavior_clone has {bc.numel()} entries, expected {n}")
+        bc = (bc.reshape(n) != 0).to(torch.uint8)
+    # The teacher reads only the env states, so tick t's labels are computed on a
+    # side stream while the student's act(t) runs on the main stream.
+    main = torch.cuda.current_stream(dev)
+    side = None
+    if not is_eval:
+        side = getattr(sim, "_teacher_stream", None)
+        if side is None:                         # created once per simulator (costly)
+            side = sim._teacher_stream = torch.cuda.Stream(dev)
+    labels_ready = getattr(sim, "_teacher_event", None)
+    if labels_ready is None:
+        labels_ready = sim._teacher_event = torch.cuda.Event()
+
+    def launch_teacher():
+        side.wait_stream(main)                   # after the previous step (and receive's copy)
+        with torch.cuda.stream(side):
+            sim.teacher(action_out=ref)          # done (frozen) envs get -1
+        labels_ready.record(side)
+
+    if not is_eval:
+        launch_teacher()
+    t_loop = time.perf_counter()
     t = 0
     while True:
         actions = act(obs, t)
@@ -100,45 +124,63 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
             actions = torch.as_tensor(np.asarray(actions), device=dev)
         actions = actions.to(device=dev, dtype=torch.int32).reshape(n)
         if not is_eval:
-            live = ~done_b
-            sim.teacher(slots=torch.where(live, slot_ids, -1), action_out=ref)
-            interactions += live.sum()
-            actions = torch.where(bc, ref, actions)
-        seqs[t] = torch.where(done_b, -1, actions)
+            main.wait_event(labels_ready)
         if keep_obs:
             obs = obs_hist[t + 1]
-        sim.step(actions, tick=t, autoreset=False, obs=obs, done=done, success=success)
-        torch.ne(done, 0, out=done_b)
-        if not is_eval:
-            steps += (~done_b).sum()
-            if receive is not None:
-                receive(ref.clone())
+        sim.step(actions, tick=t, autoreset=False, obs=obs, success=success,
+                 ref_actions=None if is_eval else ref, behavior_clone=bc,
+                 action_record=seqs[t], any_live=live[t:t + 1])
+        if not is_eval and receive is not None:
+            receive(ref.clone())
         t += 1
-        if t >= T or bool(done_b.all()):
-            # every env is done once its timer reaches 0 (imitation.py:62-63)
+        if not is_eval and t < T:
+            launch_teacher()                     # speculative: all -1 if every env is done
+        # every env is done once its timer reaches 0 (imitation.py:42, 62-63)
+        if t >= T or int(live[t - 1]) == 0:
             break
-    sim.check()
-    if bool((success < 0).any()):
-        raise RolloutError("satisfies() returned None for a finished episode (imitation.py:68)")
-
+    if not is_eval:
+        main.wait_stream(side)
+    t_end_loop = time.perf_counter()
     # distances (imitation.py:79-91): failed get tasks, initial grid at the final pose
-    get_ids = [i for i, tk in enumerate(sim.task_manager.tasks) if tk.goal_name == GOAL_GET]
-    is_get = torch.isin(task, torch.as_tensor(get_ids, dtype=torch.int32, device=dev))
+    get_ids = getattr(sim, "_get_task_ids", None)
+    if get_ids is None:
+        get_ids = sim._get_task_ids = torch.as_tensor(
+            [i for i, tk in enumerate(sim.task_manager.tasks) if tk.goal_name == GOAL_GET],
+            dtype=torch.int32, device=dev)
+    is_get = torch.isin(task, get_ids)
     probe = is_get & (success == 0)
+    # one read-back for: stats since the reset (env-steps = envs live at the start
+    # of each tick = num_interactions, imitation.py:54; minus episodes ended =
+    # transitions = num_steps, :71), a None success, any distance to compute
+    summary = torch.cat([sim.stats(), (success < 0).any().reshape(1).to(torch.int64),
+                         probe.any().reshape(1).to(torch.int64)]).cpu().tolist()
+    _, ended, env_steps, bad_success, any_probe = summary
+    num_interactions = 0 if is_eval else env_steps
+    num_steps = 0 if is_eval else env_steps - ended
     distances = torch.where(is_get, 0, -1).to(torch.int32)
-    if bool(probe.any()):
-        st = sim.get_state()
+    lens = None
+    if any_probe:
+        st = sim.get_state(fields=("agent",))
         sim.set_state(torch.stack(spec, dim=1), st["agent"])
         lens = torch.empty(n, dtype=torch.int32, device=dev)
         sim.teacher(slots=torch.where(probe, slot_ids, -1), path_len_out=lens)
-        sim.check()
+    sim.check()                                  # errors latched in the loop or the probe
+    if bad_success:
+        raise RolloutError("satisfies() returned None for a finished episode (imitation.py:68)")
+    if lens is not None:
         if bool((probe & (lens < 0)).any()):
             raise RolloutError("find_closest_resources found no target: len(None) (imitation.py:88-89)")
         distances = torch.where(probe, lens, distances)
     n_actions = (seqs >= 0).sum(dim=0).to(torch.int32)
+    if timing is not None:
+        torch.cuda.synchronize(dev)
+        t_done = time.perf_counter()
+        for k, v in (("setup", t_loop - t_start), ("loop", t_end_loop - t_loop),
+                     ("summary", t_done - t_end_loop), ("ticks", t)):
+            timing[k] = timing.get(k, 0) + v
     return RolloutInfo(action_seqs=seqs[:t], n_actions=n_actions, success=success,
-                       distances=distances, is_get=is_get, num_interactions=int(interactions),
-                       num_steps=int(steps), ticks=t,
+                       distances=distances, is_get=is_get, num_interactions=num_interactions,
+                       num_steps=num_steps, ticks=t,
                        obs=obs_hist[:t + 1] if keep_obs else None)
 
 
@@ -151,7 +193,8 @@ class ImitationRollout:
     (config.trainer.policy_mix, config.random)."""
 
     def __init__(self, world, pool, device=None, recipes=None, hints=None,
-                 max_timesteps=40, policy_mix_rate=1.0, random=None):
+                 max_timesteps=40, policy_mix_rate=1.0, random=None, obs_format="f32"):
+        self.obs_format = obs_format
         self.world, self.device = world, device
         self.recipes, self.hints, self.max_timesteps = recipes, hints, max_timesteps
         self.pool = np.asarray(pool, dtype=np.uint8)
@@ -166,6 +209,7 @@ class ImitationRollout:
                          pool_capacity=max(1, len(self.pool)), recipes=self.recipes,
                          hints=self.hints, max_timesteps=self.max_timesteps)
             s.load_pool(self.pool)
+            s.set_obs_format(self.obs_format)
             self._sims[n] = s
         return s
 

@@ -60,6 +60,7 @@ class CraftSim:
                                          self.env_id_base, self.pool_capacity,
                                          ctypes.byref(handle)), what="craft_sim_create")
         self._h = handle
+        self.obs_format, self.obs_dtype = "f32", torch.float32
 
     # ---- lifetime ---------------------------------------------------------------
     def close(self):
@@ -78,6 +79,16 @@ class CraftSim:
         1 nontemporal, 2 write-through); results are identical for every setting."""
         self._check(N.lib().craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu),
                                            int(obs_store)), "craft_sim_tune")
+
+    _OBS_FORMATS = {"f32": (N.OBS_F32, torch.float32), "bf16": (N.OBS_BF16, torch.bfloat16),
+                    "u8": (N.OBS_U8, torch.uint8)}
+
+    def set_obs_format(self, fmt):
+        """Element type of every observation this simulator writes: "f32"
+        (default), "bf16" or "u8" — the same exact integer values in each."""
+        code, dtype = self._OBS_FORMATS[fmt]
+        self._check(N.lib().craft_sim_set_obs_format(self._h, code), "craft_sim_set_obs_format")
+        self.obs_format, self.obs_dtype = fmt, dtype
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -106,7 +117,12 @@ class CraftSim:
 
     def empty_obs(self, n=None):
         n = self.n_envs if n is None else n
-        return torch.empty((n, self.n_features), dtype=torch.float32, device=self.device)
+        return torch.empty((n, self.n_features), dtype=self.obs_dtype, device=self.device)
+
+    def _obs(self, obs):
+        if obs is not None and obs.dtype != self.obs_dtype:
+            raise TypeError(f"obs is {obs.dtype}, the simulator writes {self.obs_dtype}")
+        return _ptr(obs)
 
     # ---- scenario pool -----------------------------------------------------------------
     def load_pool(self, grids, first=0):
@@ -129,19 +145,56 @@ class CraftSim:
         n = self.n_envs
         args = [self._i32(a, n) for a in (scenario, pos_x, pos_y, dir, task)]
         self._args_keepalive = args
-        self._check(N.lib().craft_reset(self._h, *[_ptr(a) for a in args], _ptr(obs), self._stream()),
+        self._check(N.lib().craft_reset(self._h, *[_ptr(a) for a in args], self._obs(obs), self._stream()),
                     "craft_reset")
         return obs
 
     def step(self, actions=None, seed=0, tick=0, autoreset=True, obs=None, reward=None, done=None,
-             success=None):
-        """One rollout tick for every slot (see include/craft.h craft_step).
-        actions: int32 device tensor [N] or None for the in-kernel hashed draw."""
-        a = self._i32(actions, self.n_envs) if actions is not None else None
+             success=None, ref_actions=None, behavior_clone=None, action_record=None,
+             any_live=None):
+        """One rollout tick for every slot (include/craft.h craft_step / craft_step_ex).
+        actions: int32 device tensor [N] or None for the in-kernel hashed draw;
+        ref_actions + behavior_clone (uint8 [N]): cloned actions; action_record
+        (int32 [N]) receives the action taken (-1 for done slots); any_live (a
+        one-element int32 device tensor) is set to 1 if a slot is still running."""
+        n = self.n_envs
         flags = N.STEP_AUTORESET if autoreset else 0
-        self._check(N.lib().craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
-                                       int(tick), flags, _ptr(obs), _ptr(reward), _ptr(done),
-                                       _ptr(success), self._stream()), "craft_step")
+        if ref_actions is None and behavior_clone is None and action_record is None \
+                and any_live is None:
+            # plain tick: the short craft_step entry (least host overhead per launch)
+            a = self._i32(actions, n) if actions is not None else None
+            self._check(N.lib().craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
+                                           int(tick), flags, self._obs(obs), _ptr(reward),
+                                           _ptr(done), _ptr(success), self._stream()), "craft_step")
+            return obs
+        args = N.craft_step_args_t()
+        keep = []
+
+        def put(field, t):
+            if t is not None:
+                keep.append(t)
+                setattr(args, field, t.data_ptr())
+
+        put("actions", self._i32(actions, n) if actions is not None else None)
+        put("ref_actions", self._i32(ref_actions, n) if ref_actions is not None else None)
+        if behavior_clone is not None:
+            bc = torch.as_tensor(behavior_clone, device=self.device)
+            bc = (bc != 0).to(torch.uint8).contiguous() if bc.dtype != torch.uint8 else bc.contiguous()
+            if bc.numel() != n:
+                raise ValueError(f"behavior_clone: expected {n} entries")
+            put("behavior_clone", bc)
+        for name, t, dt in (("reward", reward, torch.float32), ("done", done, torch.uint8),
+                            ("success", success, torch.int8), ("action_record", action_record, torch.int32),
+                            ("any_live", any_live, torch.int32)):
+            if t is not None and (t.dtype != dt or not t.is_contiguous()):
+                raise TypeError(f"{name} must be a contiguous {dt} tensor")
+            put(name, t)
+        self._obs(obs)
+        put("obs", obs)
+        args.action_seed = seed & (2**64 - 1)
+        args.tick = int(tick)
+        args.flags = flags
+        self._check(N.lib().craft_step_ex(self._h, ctypes.byref(args), self._stream()), "craft_step")
         return obs
 
     def stats(self, reset=False, out=None):
@@ -164,7 +217,7 @@ class CraftSim:
         s = self._i32(slots)
         n = s.numel() if s is not None else (self.n_envs if n is None else n)
         t = self._i32(tasks, n)
-        self._check(N.lib().craft_observe(self._h, _ptr(s), n, _ptr(t), _ptr(obs), _ptr(sat),
+        self._check(N.lib().craft_observe(self._h, _ptr(s), n, _ptr(t), self._obs(obs), _ptr(sat),
                                           self._stream()), "craft_observe")
         return obs, sat
 
@@ -178,17 +231,19 @@ class CraftSim:
                                           _ptr(path_len_out), self._stream()), "craft_teacher")
         return action_out, path_len_out
 
-    def get_state(self, slots=None, n=None):
+    def get_state(self, slots=None, n=None, fields=("agent", "inventory", "grid", "spec")):
+        """Device copies of the requested fields: agent int32 [n, 4] (x, y, dir,
+        timer), inventory int32 [n, K], grid uint8 [n, W*H], spec int32 [n, 5]."""
         s = self._i32(slots)
         n = s.numel() if s is not None else (self.n_envs if n is None else n)
         dev = self.device
-        agent = torch.empty((n, 4), dtype=torch.int32, device=dev)
-        inv = torch.empty((n, self.n_kinds), dtype=torch.int32, device=dev)
-        grid = torch.empty((n, self.width * self.height), dtype=torch.uint8, device=dev)
-        spec = torch.empty((n, 5), dtype=torch.int32, device=dev)
-        self._check(N.lib().craft_get_state(self._h, _ptr(s), n, _ptr(agent), _ptr(inv), _ptr(grid),
-                                            _ptr(spec), self._stream()), "craft_get_state")
-        return dict(agent=agent, inventory=inv, grid=grid, spec=spec)
+        shapes = {"agent": ((n, 4), torch.int32), "inventory": ((n, self.n_kinds), torch.int32),
+                  "grid": ((n, self.width * self.height), torch.uint8), "spec": ((n, 5), torch.int32)}
+        out = {f: torch.empty(shapes[f][0], dtype=shapes[f][1], device=dev) for f in fields}
+        self._check(N.lib().craft_get_state(self._h, _ptr(s), n, _ptr(out.get("agent")),
+                                            _ptr(out.get("inventory")), _ptr(out.get("grid")),
+                                            _ptr(out.get("spec")), self._stream()), "craft_get_state")
+        return out
 
     def set_state(self, spec, agent, inventory=None, slots=None):
         sp = self._i32(spec)

@@ -311,25 +311,31 @@ def test_pool_rejects_open_border():
 @pytest.mark.parametrize("window", [3, 5])
 def test_tuning_does_not_change_results(window):
     """craft_sim_tune changes only the kernel geometry: every tile size and
-    residency cap gives bit-identical observations, states and statistics."""
+    residency cap gives bit-identical observations, states and statistics; the
+    bf16 and u8 observation formats hold exactly the same values."""
     world = world_for(12, window)
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 128)
     n = 5000   # not a multiple of any tile: exercises the partial last tile
     specs = synthetic_specs(pool, 12, 12, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
     ref = None
-    for tile, cap, pol in [(64, 0, 0), (32, 0, 1), (16, 0, 2), (16, 6, 0), (32, 4, 2), (64, 3, 1)]:
+    for tile, cap, pol, fmt in [(64, 0, 0, "f32"), (32, 0, 1, "f32"), (16, 0, 2, "f32"),
+                                (16, 6, 0, "f32"), (32, 4, 2, "f32"), (64, 3, 1, "f32"),
+                                (64, 0, 1, "bf16"), (16, 0, 0, "bf16"), (64, 0, 1, "u8"),
+                                (32, 0, 2, "u8")]:
         sim = sim_with_pool(world, n, pool)
         sim.tune(tile, cap, pol)
-        sim.reset(*specs)
+        sim.set_obs_format(fmt)
         obs = sim.empty_obs()
-        outs = []
+        assert obs.dtype == {"f32": torch.float32, "bf16": torch.bfloat16, "u8": torch.uint8}[fmt]
+        sim.reset(*specs, obs=obs)
+        outs = [host(obs.float())]
         for t in range(12):
             sim.step(seed=4, tick=t, obs=obs)
-            outs.append(host(obs).copy())
+            outs.append(host(obs.float()))
         o2 = sim.empty_obs()
         sim.observe(obs=o2, n=n)
-        outs.append(host(o2))
+        outs.append(host(o2.float()))
         st = {k: host(v) for k, v in sim.get_state().items()}
         stats = host(sim.stats())
         sim.check()
@@ -337,7 +343,7 @@ def test_tuning_does_not_change_results(window):
             ref = (outs, st, stats)
         else:
             for a, b in zip(outs, ref[0]):
-                np.testing.assert_array_equal(a, b, err_msg=f"tile {tile} cap {cap}")
+                np.testing.assert_array_equal(a, b, err_msg=f"tile {tile} cap {cap} {fmt}")
             for k in st:
                 np.testing.assert_array_equal(st[k], ref[1][k])
             np.testing.assert_array_equal(stats, ref[2])

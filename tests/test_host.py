@@ -207,3 +207,19 @@ def test_dataset_reads_reference_split_files(golden):
         assert np.array_equal(ds.pool_array()[spec[:, 0]], fx[f"{split}_grids"][fx[f"{split}_world"]])
         L = fx[f"{split}_actions"]
         assert all(tuple(int(a) for a in L[i] if a >= 0) == it["ref_actions"] for i, it in enumerate(ds))
+
+
+def test_step_args_layout_matches_c(tmp_path):
+    """ctypes craft_step_args_t == the C struct of include/craft.h (offsets, size)."""
+    import subprocess
+    fields = [f for f, _ in N.craft_step_args_t._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "craft.h"\nint main(void){\n'
+                   + "".join(f'printf("%zu\\n", offsetof(craft_step_args_t, {f}));\n' for f in fields)
+                   + 'printf("%zu\\n", sizeof(craft_step_args_t));\nreturn 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(N._HERE, "..", "include"),
+                           "-o", str(exe), str(src)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    want = [getattr(N.craft_step_args_t, f).offset for f in fields] + [ctypes.sizeof(N.craft_step_args_t)]
+    assert got == want
