@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--world", default="craft_medium_12x12")
     p.add_argument("--pool", type=int, default=1024)
     p.add_argument("--ring", type=int, default=4, help="observation buffers cycled per tick")
+    p.add_argument("--tile", type=int, default=0, help="envs per workgroup (0 = default)")
+    p.add_argument("--obs-store", type=int, default=1, help="0 write-back, 1 nontemporal, 2 sc1")
+    p.add_argument("--ticks-per-launch", type=int, default=1,
+                   help="K > 1: craft_rollout runs K ticks per launch (same work per tick)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -85,26 +89,36 @@ def main():
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
+    sim.tune(args.tile, 0, args.obs_store)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
     specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
                             task_ids=tasks)
     sim.reset(*specs)
     F = sim.n_features
-    ring = [sim.empty_obs() for _ in range(args.ring)]
-    reward = torch.empty(n, dtype=torch.float32, device=dev)
-    done = torch.empty(n, dtype=torch.uint8, device=dev)
-    success = torch.empty(n, dtype=torch.int8, device=dev)
+    R, K = args.ring, max(1, args.ticks_per_launch)
+    if args.steps % K or args.warmup % K:
+        raise SystemExit("--steps and --warmup must be multiples of --ticks-per-launch")
+    ring = torch.empty((R, n, F), dtype=sim.obs_dtype, device=dev)     # one tick's obs per slot
+    reward = torch.empty((R, n), dtype=torch.float32, device=dev)
+    done = torch.empty((R, n), dtype=torch.uint8, device=dev)
+    success = torch.empty((R, n), dtype=torch.int8, device=dev)
 
     tick = 0
 
-    def step():
+    def launch():
+        """K ticks: one craft_step (K = 1) or one craft_rollout launch."""
         nonlocal tick
-        sim.step(seed=args.seed, tick=tick, obs=ring[tick % args.ring], reward=reward, done=done,
-                 success=success)
-        tick += 1
+        if K == 1:
+            r = tick % R
+            sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r], done=done[r],
+                     success=success[r])
+        else:
+            sim.rollout(K, seed=args.seed, tick0=tick, obs=ring, reward=reward, done=done,
+                        success=success)
+        tick += K
 
-    for _ in range(args.warmup):
-        step()
+    for _ in range(args.warmup // K):
+        launch()
     sim.check()
 
     def barrier():
@@ -114,23 +128,23 @@ def main():
     # ---- timed region: K ticks, barrier + synchronize on both sides ------------------
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for _ in range(args.steps // K):
+        launch()
     barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
 
     # ---- per-launch kernel duration, HIP events on the launch stream --------------------
     kstream = torch.cuda.current_stream(dev)
-    m = min(args.steps, 400)
+    m = max(1, min(args.steps // K, 400))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(m)]
     torch.cuda.synchronize()
     for a, b in evs:
         a.record(kstream)
-        step()
+        launch()
         b.record(kstream)
     torch.cuda.synchronize()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))     # per launch (K ticks)
 
     # ---- scalar episode summary: one RCCL all-reduce of int64[3] --------------------------
     stats = D.reduce_episode_stats(sim.stats()).cpu().tolist()
@@ -140,9 +154,12 @@ def main():
         total_steps = n * world_size * args.steps
         value = total_steps / elapsed
         bps = bytes_per_env_step(sim.width, sim.height, sim.params["WINDOW_WIDTH"], F)
-        achieved = bps * n / (kernel_ms * 1e-3) / 1e9
+        tile = args.tile or {3: 64, 5: 32}.get(sim.params["WINDOW_WIDTH"], 16)
+        achieved = bps * n * K / (kernel_ms * 1e-3) / 1e9
         traffic = None
         workload = f"{args.world}_w{sim.params['WINDOW_WIDTH']}_B{n}_random_rollout_full_features"
+        if K > 1:
+            workload += f"_K{K}"
         if os.path.exists(args.traffic):
             try:
                 tj = json.load(open(args.traffic))
@@ -168,12 +185,14 @@ def main():
                        "global_batch": n * world_size, "window": sim.params["WINDOW_WIDTH"],
                        "n_features": F, "obs_dtype": "fp32", "obs_ring": args.ring,
                        "pool": args.pool, "parallelism": f"env-shard x{world_size}",
-                       "max_timesteps": sim.config.max_timesteps},
+                       "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, "
-                                   f"{ {3: 64, 5: 32}.get(sim.params['WINDOW_WIDTH'], 16)}>",
-                         "kernel_us": kernel_ms * 1e3, "bytes_per_env_step": bps},
+                         "kernel": (f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, {tile}>"
+                                    if K == 1 else
+                                    f"rollout_kernel<{sim.params['WINDOW_WIDTH']}, {tile}>"),
+                         "kernel_us": kernel_ms * 1e3, "ticks_per_launch": K,
+                         "bytes_per_launch": bps * n * K, "bytes_per_env_step": bps},
             "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},
         }
         if world_size == 1 and not args.no_cpu_baseline:

@@ -234,6 +234,18 @@ typedef struct {
 } craft_step_args_t;
 int craft_step_ex(craft_sim_t* sim, const craft_step_args_t* args, void* stream);
 
+/* n_ticks consecutive craft_step ticks (tick0, tick0+1, ...) in one launch, with
+ * results identical to n_ticks craft_step calls: each workgroup keeps its envs
+ * on chip between ticks, so the per-tick prologue overlaps other workgroups'
+ * observation stores.  For rollouts whose actions do not depend on the
+ * observations: `actions` is device int32[n_ticks][n_envs] or NULL for the
+ * hashed draw.  Tick t writes ring slot t % ring of each output: obs
+ * [ring][n_envs][n_features] (obs format; each slot 16-byte aligned), reward /
+ * done / success [ring][n_envs]; each may be NULL. */
+int craft_rollout(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed, int64_t tick0,
+                  int32_t n_ticks, uint32_t flags, void* obs, int32_t ring, float* reward,
+                  uint8_t* done, int8_t* success, void* stream);
+
 /* Sums the episode statistics accumulated by craft_step into stats_out
  * (device int64[3] = {successes, episodes ended, env-steps}) — the scalar
  * summary a multi-GPU run all-reduces over RCCL.  reset != 0 zeroes the

@@ -92,6 +92,19 @@ struct TileArgs {
   int32_t* any_live;
 };
 
+struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
+  const int32_t* actions;  // [n_ticks][n_envs] or null (hashed draw)
+  uint64_t seed;
+  int64_t tick0;
+  int32_t n_ticks;
+  int32_t ring;            // outputs of tick t go to ring slot t % ring
+  uint32_t flags;
+  void* obs;               // [ring][n_envs][F] in the obs format, or null
+  float* reward;           // [ring][n_envs] each, or null
+  uint8_t* done;
+  int8_t* sat;
+};
+
 struct Agent {
   int x, y, dir, frozen, timer, scen, task;
 };

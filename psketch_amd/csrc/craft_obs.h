@@ -1,0 +1,150 @@
+// craft_obs.h — the observation half of a tick, shared by the tick kernel
+// (craft_tile.hip) and the multi-tick rollout kernel (craft_rollout.hip):
+// D scatters CraftState.features() (craft.py:296-330) of each env of a tile into
+// u8 rows in LDS, E streams the rows to HBM in the handle's observation format.
+#pragma once
+#include "craft_device.h"
+
+namespace craft {
+
+typedef unsigned int obs_vec __attribute__((ext_vector_type(4)));
+
+// Kind id at (cx, cy) of an LDS grid row as a one-hot bit, 0 outside the grid
+// (pad_slice's zero padding, misc/array.py:3-25).
+__device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int cx, int cy) {
+  const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+  const int xc = min(max(cx, 0), W - 1), yc = min(max(cy, 0), H - 1);
+  const int k = g[xc * H + yc];
+  return ok ? (1u << k) : 0u;
+}
+
+// 16 bytes of output from the tile's u8 feature rows: 4 fp32 (v_cvt_f32_ubyte),
+// 8 bf16 (the high half of the exact fp32 value of a byte) or 16 u8.
+template <int FMT>
+__device__ __forceinline__ obs_vec pack16(const uint8_t* s_obs, int sidx) {
+  if (FMT == CRAFT_OBS_F32) {
+    const uint32_t w = reinterpret_cast<const uint32_t*>(s_obs)[sidx];
+    return obs_vec{__float_as_uint((float)(w & 0xff)), __float_as_uint((float)((w >> 8) & 0xff)),
+                   __float_as_uint((float)((w >> 16) & 0xff)), __float_as_uint((float)(w >> 24))};
+  } else if (FMT == CRAFT_OBS_BF16) {
+    const uint2 w = reinterpret_cast<const uint2*>(s_obs)[sidx];
+    auto bf = [](uint32_t b) { return __float_as_uint((float)b) >> 16; };
+    auto two = [&](uint32_t x) { return bf(x & 0xff) | (bf((x >> 8) & 0xff) << 16); };
+    return obs_vec{two(w.x), two(w.x >> 16), two(w.y), two(w.y >> 16)};
+  } else {
+    const uint4 w = reinterpret_cast<const uint4*>(s_obs)[sidx];
+    return obs_vec{w.x, w.y, w.z, w.w};
+  }
+}
+
+// Phase E: the tile's rows are contiguous in the output, so the whole tile is one
+// flat stream of 16-byte buffer stores (32-bit offsets off one wave-uniform
+// descriptor); the cache policy is a tuning knob (craft_sim_tune).  NTHR threads
+// (tid in [0, NTHR)) share the stream; with ZERO they also clear every byte they
+// read, leaving the rows zeroed for the next scatter.
+template <int FMT, int NTHR = kThreads, bool ZERO = false>
+__device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t env0, int F, int nE,
+                                           int policy, int tid) {
+  constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
+  constexpr int PER = 16 / ESZ;                // values per 16-byte store
+  const int total = nE * F;
+  const int nv = total / PER;
+  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
+  constexpr int U = 4;                         // independent 16-byte stores in flight per lane
+  for (int base = tid; base < nv; base += U * NTHR) {
+    obs_vec o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sidx = base + u * NTHR;
+      if (sidx < nv) {
+        o[u] = pack16<FMT>(s_obs, sidx);
+        if (ZERO) {
+          if (FMT == CRAFT_OBS_F32) reinterpret_cast<uint32_t*>(s_obs)[sidx] = 0u;
+          else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint2*>(s_obs)[sidx] = make_uint2(0u, 0u);
+          else reinterpret_cast<uint4*>(s_obs)[sidx] = make_uint4(0u, 0u, 0u, 0u);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sidx = base + u * NTHR;
+      if (sidx < nv) {
+        if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 2);         // nt
+        else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 16);   // sc1
+        else __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 0);
+      }
+    }
+  }
+  for (int f = nv * PER + tid; f < total; f += NTHR) {       // the last few values of the tile
+    const uint32_t b = s_obs[f];
+    if (ZERO) s_obs[f] = 0;
+    if (FMT == CRAFT_OBS_F32) reinterpret_cast<float*>(tile_out)[f] = (float)b;
+    else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint16_t*>(tile_out)[f] = (uint16_t)(__float_as_uint((float)b) >> 16);
+    else tile_out[f] = (uint8_t)b;
+  }
+}
+
+// Phase D: all threads scatter the non-zero bytes of each env's features() row
+// into the zeroed u8 rows s_obs[TILE][F]: local one-hots, block-max-pooled
+// one-hots, inventory counts, dir one-hot.  s_agent[e] = x | y<<8 | dir<<16 | 1<<24
+// for a live env (0 = skip).
+template <int WIN, int TILE>
+__device__ __forceinline__ void scatter_features(const SimView& v, const uint8_t* s_grid,
+                                                 const uint8_t* s_inv, const uint32_t* s_agent,
+                                                 uint8_t* s_obs, int nE, int tid) {
+  constexpr int kParts = kThreads / TILE;        // threads per env
+  const int F = v.F;
+  {
+    const int e = tid % TILE, part = tid / TILE;
+    const uint32_t ag = s_agent[e];
+    if (e < nE && (ag >> 24)) {
+      const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+      const uint8_t* g = s_grid + e * v.GS;
+      uint8_t* row = s_obs + e * F;
+      const int W = v.W, H = v.H, K = v.K;
+      constexpr int W2 = WIN * WIN;
+      const int L = W2 * K;
+      if (part == 0) {
+        constexpr int hw = WIN / 2;
+#pragma unroll
+        for (int i = 0; i < WIN; ++i)
+#pragma unroll
+          for (int j = 0; j < WIN; ++j) {
+            const int cx = x - hw + i, cy = y - hw + j;
+            if ((unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H) {
+              const int k = g[cx * H + cy];
+              if (k) row[(i * WIN + j) * K + k] = 1;                   // local one-hot
+            }
+          }
+        const uint8_t* iv = s_inv + e * kInvStride;
+        for (int k = 0; k < K; ++k) row[2 * L + k] = iv[k];           // inventory counts
+        row[2 * L + K + dir] = 1;                                      // dir one-hot
+      } else {
+        constexpr int bh = W2 / 2;
+#pragma unroll
+        for (int j = 0; j < (W2 + kParts - 2) / (kParts - 1); ++j) {
+          const int b = part - 1 + (kParts - 1) * j;
+          if (b >= W2) break;
+          const int bi = b / WIN, bj = b - bi * WIN;
+          const int x0 = x - bh + bi * WIN, y0 = y - bh + bj * WIN;
+          uint32_t msk = 0;
+          if (x0 < W && x0 + WIN > 0 && y0 < H && y0 + WIN > 0) {
+#pragma unroll
+            for (int ii = 0; ii < WIN; ++ii)
+#pragma unroll
+              for (int jj = 0; jj < WIN; ++jj) msk |= cell_bit(g, W, H, x0 + ii, y0 + jj);
+          }
+          msk &= ~1u;                                                  // kind 0 = empty
+          uint8_t* brow = row + L + b * K;
+          while (msk) {                                                // block-max-pooled one-hot
+            brow[__ffs(msk) - 1] = 1;
+            msk &= msk - 1;
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace craft

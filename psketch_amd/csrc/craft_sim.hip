@@ -1,6 +1,7 @@
 // craft_sim.hip — host side of the C ABI (include/craft.h): handle lifetime,
 // scenario pool, launches, state I/O and episode statistics.
-// Kernels: craft_tile.hip (tick / transition / observe / reset), craft_teacher.hip.
+// Kernels: craft_tile.hip (tick / transition / observe / reset), craft_rollout.hip
+// (multi-tick), craft_teacher.hip.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -13,6 +14,8 @@ hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const Tile
                        hipStream_t st);
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st);
+hipError_t launch_rollout(int win, int tile, const SimView& v, const RolloutArgs& a, size_t lds,
+                          hipStream_t st);
 
 namespace {
 
@@ -483,6 +486,32 @@ int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
   a.rec = x->action_record;
   a.any_live = x->any_live;
   return launch(s, craft::MODE_TICK, a, stream, "craft_step launch");
+}
+
+int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, int64_t tick0,
+                  int32_t n_ticks, uint32_t flags, void* obs, int32_t ring, float* reward,
+                  uint8_t* done, int8_t* success, void* stream) {
+  if (!s) return CRAFT_EINVAL;
+  if (n_ticks < 0 || ring < 1 || tick0 < 0)
+    return fail(s, CRAFT_EINVAL, "craft_rollout: need n_ticks >= 0, ring >= 1, tick0 >= 0");
+  const int esz = s->view.obs_fmt == CRAFT_OBS_F32 ? 4 : (s->view.obs_fmt == CRAFT_OBS_BF16 ? 2 : 1);
+  if (obs && (!aligned16(obs) || (ring > 1 && (s->n_envs * (int64_t)s->view.F * esz) % 16 != 0)))
+    return fail(s, CRAFT_EINVAL, "craft_rollout: every obs ring slot must be 16-byte aligned");
+  craft::RolloutArgs a{};
+  a.actions = actions;
+  a.seed = action_seed;
+  a.tick0 = tick0;
+  a.n_ticks = n_ticks;
+  a.ring = ring;
+  a.flags = flags;
+  a.obs = obs;
+  a.reward = reward;
+  a.done = done;
+  a.sat = success;
+  hipError_t e = craft::launch_rollout(s->cfg.window_width, s->tile, s->view, a, lds_bytes(s, s->tile),
+                                       reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");
+  return CRAFT_OK;
 }
 
 int craft_stats(craft_sim_t* s, int64_t* stats_out, int32_t reset, void* stream) {

@@ -16,7 +16,7 @@
 //      v_cvt_f32_ubyte; bf16: 8 bytes; u8: 16 bytes as they are).
 // The kernel is bound by E's HBM writes (F*4 = 1616 B per env at w=3).  See
 // DESIGN.md for the roofline and the phase timings that shaped this layout.
-#include "craft_device.h"
+#include "craft_obs.h"
 
 namespace craft {
 
@@ -43,77 +43,8 @@ namespace craft {
 #define STAMP_END() do {} while (0)
 #endif
 
-typedef unsigned int obs_vec __attribute__((ext_vector_type(4)));
-
-// Kind id at (cx, cy) of an LDS grid row as a one-hot bit, 0 outside the grid
-// (pad_slice's zero padding, misc/array.py:3-25).
-__device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int cx, int cy) {
-  const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-  const int xc = min(max(cx, 0), W - 1), yc = min(max(cy, 0), H - 1);
-  const int k = g[xc * H + yc];
-  return ok ? (1u << k) : 0u;
-}
-
-// 16 bytes of output from the tile's u8 feature rows: 4 fp32 (v_cvt_f32_ubyte),
-// 8 bf16 (the high half of the exact fp32 value of a byte) or 16 u8.
-template <int FMT>
-__device__ __forceinline__ obs_vec pack16(const uint8_t* s_obs, int sidx) {
-  if (FMT == CRAFT_OBS_F32) {
-    const uint32_t w = reinterpret_cast<const uint32_t*>(s_obs)[sidx];
-    return obs_vec{__float_as_uint((float)(w & 0xff)), __float_as_uint((float)((w >> 8) & 0xff)),
-                   __float_as_uint((float)((w >> 16) & 0xff)), __float_as_uint((float)(w >> 24))};
-  } else if (FMT == CRAFT_OBS_BF16) {
-    const uint2 w = reinterpret_cast<const uint2*>(s_obs)[sidx];
-    auto bf = [](uint32_t b) { return __float_as_uint((float)b) >> 16; };
-    auto two = [&](uint32_t x) { return bf(x & 0xff) | (bf((x >> 8) & 0xff) << 16); };
-    return obs_vec{two(w.x), two(w.x >> 16), two(w.y), two(w.y >> 16)};
-  } else {
-    const uint4 w = reinterpret_cast<const uint4*>(s_obs)[sidx];
-    return obs_vec{w.x, w.y, w.z, w.w};
-  }
-}
-
-// Phase E: the tile's rows are contiguous in the output, so the whole tile is one
-// flat stream of 16-byte buffer stores (32-bit offsets off one wave-uniform
-// descriptor); the cache policy is a tuning knob (craft_sim_tune).
-template <int FMT>
-__device__ __forceinline__ void stream_obs(const uint8_t* s_obs, void* obs, int64_t env0, int F, int nE,
-                                           int policy, int tid) {
-  constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
-  constexpr int PER = 16 / ESZ;                // values per 16-byte store
-  const int total = nE * F;
-  const int nv = total / PER;
-  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
-  constexpr int U = 4;                         // independent 16-byte stores in flight per lane
-  for (int base = tid; base < nv; base += U * kThreads) {
-    obs_vec o[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int sidx = base + u * kThreads;
-      if (sidx < nv) o[u] = pack16<FMT>(s_obs, sidx);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int sidx = base + u * kThreads;
-      if (sidx < nv) {
-        if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 2);         // nt
-        else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 16);   // sc1
-        else __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 0);
-      }
-    }
-  }
-  for (int f = nv * PER + tid; f < total; f += kThreads) {   // the last few values of the tile
-    const uint32_t b = s_obs[f];
-    if (FMT == CRAFT_OBS_F32) reinterpret_cast<float*>(tile_out)[f] = (float)b;
-    else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint16_t*>(tile_out)[f] = (uint16_t)(__float_as_uint((float)b) >> 16);
-    else tile_out[f] = (uint8_t)b;
-  }
-}
-
 template <int WIN, int MODE, int TILE>
 __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
-  constexpr int kParts = kThreads / TILE;        // threads per env in phase D
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
   uint8_t* s_grid = smem;
@@ -336,56 +267,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   STAMP(4);
 
   // ---- D: scatter the observation's non-zero bytes ---------------------------------------------
-  {
-    const int e = tid % TILE, part = tid / TILE;
-    const uint32_t ag = s_agent[e];
-    if (e < nE && (ag >> 24)) {
-      const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
-      const uint8_t* g = s_grid + e * v.GS;
-      uint8_t* row = s_obs + e * F;
-      const int W = v.W, H = v.H, K = v.K;
-      constexpr int W2 = WIN * WIN;
-      const int L = W2 * K;
-      if (part == 0) {
-        constexpr int hw = WIN / 2;
-#pragma unroll
-        for (int i = 0; i < WIN; ++i)
-#pragma unroll
-          for (int j = 0; j < WIN; ++j) {
-            const int cx = x - hw + i, cy = y - hw + j;
-            if ((unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H) {
-              const int k = g[cx * H + cy];
-              if (k) row[(i * WIN + j) * K + k] = 1;                   // local one-hot
-            }
-          }
-        const uint8_t* iv = s_inv + e * kInvStride;
-        for (int k = 0; k < K; ++k) row[2 * L + k] = iv[k];           // inventory counts
-        row[2 * L + K + dir] = 1;                                      // dir one-hot
-      } else {
-        constexpr int bh = W2 / 2;
-#pragma unroll
-        for (int j = 0; j < (W2 + kParts - 2) / (kParts - 1); ++j) {
-          const int b = part - 1 + (kParts - 1) * j;
-          if (b >= W2) break;
-          const int bi = b / WIN, bj = b - bi * WIN;
-          const int x0 = x - bh + bi * WIN, y0 = y - bh + bj * WIN;
-          uint32_t msk = 0;
-          if (x0 < W && x0 + WIN > 0 && y0 < H && y0 + WIN > 0) {
-#pragma unroll
-            for (int ii = 0; ii < WIN; ++ii)
-#pragma unroll
-              for (int jj = 0; jj < WIN; ++jj) msk |= cell_bit(g, W, H, x0 + ii, y0 + jj);
-          }
-          msk &= ~1u;                                                  // kind 0 = empty
-          uint8_t* brow = row + L + b * K;
-          while (msk) {                                                // block-max-pooled one-hot
-            brow[__ffs(msk) - 1] = 1;
-            msk &= msk - 1;
-          }
-        }
-      }
-    }
-  }
+  scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
   __syncthreads();
   STAMP(5);
 

@@ -197,6 +197,35 @@ class CraftSim:
         self._check(N.lib().craft_step_ex(self._h, ctypes.byref(args), self._stream()), "craft_step")
         return obs
 
+    def rollout(self, n_ticks, seed=0, tick0=0, actions=None, autoreset=True, obs=None,
+                reward=None, done=None, success=None):
+        """n_ticks craft_step ticks in one launch (include/craft.h craft_rollout),
+        identical to calling step(tick=tick0 + k) n_ticks times.  actions: int32
+        [n_ticks, N] or None (hashed); obs: [R, N, F] ring in the obs format
+        (tick t writes obs[t % R]); reward / done / success: [R, N] rings."""
+        n = self.n_envs
+        if obs is not None and (obs.dim() != 3 or obs.shape[1:] != (n, self.n_features)):
+            raise ValueError(f"obs must be [ring, {n}, {self.n_features}]")
+        ring = obs.shape[0] if obs is not None else None
+        for name, t, dt in (("reward", reward, torch.float32), ("done", done, torch.uint8),
+                            ("success", success, torch.int8)):
+            if t is None:
+                continue
+            if t.dtype != dt or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != n:
+                raise TypeError(f"{name} must be a contiguous {dt} tensor [ring, {n}]")
+            if ring is not None and t.shape[0] != ring:
+                raise ValueError(f"{name} ring {t.shape[0]} != obs ring {ring}")
+            ring = t.shape[0]
+        a = None
+        if actions is not None:
+            a = self._i32(actions, n * n_ticks)
+        self._check(N.lib().craft_rollout(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
+                                          int(tick0), int(n_ticks),
+                                          N.STEP_AUTORESET if autoreset else 0, self._obs(obs),
+                                          int(ring or 1), _ptr(reward), _ptr(done), _ptr(success),
+                                          self._stream()), "craft_rollout")
+        return obs
+
     def stats(self, reset=False, out=None):
         """Device int64[3] {successes, episodes ended, env-steps}."""
         if out is None:

@@ -379,3 +379,57 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
             rc, a = o.teacher(envs[i:i + 1], int(specs[4][i]))
             assert (a if rc == 0 else -2) == act[i], i
     sim.check()
+
+
+@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given", [
+    ("craft_medium_12x12", 12, 0, "f32", True, False),
+    ("craft_medium_12x12", 12, 16, "bf16", True, True),
+    ("craft_medium_12x12", 12, 32, "u8", False, True),
+    ("craft_medium_12x12_w5", 12, 0, "f32", True, False),
+    ("craft_16x16_w7", 16, 0, "f32", False, False),
+    ("craft_medium", 8, 64, "f32", True, True)])
+def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given):
+    """craft_rollout(K ticks) == K craft_step calls: observation / reward / done /
+    success rings, final states and episode statistics, bit for bit; several
+    launches in a row (state written back and picked up again)."""
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 64)
+    n = 5000                                   # a partial last tile
+    specs = synthetic_specs(pool, W, W, n, 0, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
+    R, chunks = 3, [5, 1, 9]
+    T = sum(chunks)
+    rng = np.random.RandomState(4)
+    acts = torch.as_tensor(rng.randint(0, 6, size=(T, n)).astype(np.int32), device="cuda")
+    sims = []
+    for _ in range(2):
+        sim = sim_with_pool(world, n, pool)
+        sim.tune(tile, 0, 1)
+        sim.set_obs_format(fmt)
+        sim.reset(*specs)
+        sims.append(sim)
+    a, b = sims
+    ring = lambda shape, dt: torch.zeros((R,) + shape, dtype=dt, device="cuda")  # noqa: E731
+    oa, ob = ring((n, a.n_features), a.obs_dtype), ring((n, a.n_features), a.obs_dtype)
+    outs = {k: (ring((n,), dt), ring((n,), dt)) for k, dt in
+            (("reward", torch.float32), ("done", torch.uint8), ("success", torch.int8))}
+    t0 = 0
+    for K in chunks:
+        a.rollout(K, seed=11, tick0=t0, actions=acts[t0:t0 + K] if given else None,
+                  autoreset=autoreset, obs=oa, reward=outs["reward"][0], done=outs["done"][0],
+                  success=outs["success"][0])
+        for k in range(K):
+            t = t0 + k
+            b.step(acts[t] if given else None, seed=11, tick=t, autoreset=autoreset, obs=ob[t % R],
+                   reward=outs["reward"][1][t % R], done=outs["done"][1][t % R],
+                   success=outs["success"][1][t % R])
+        t0 += K
+        np.testing.assert_array_equal(host(oa.float()), host(ob.float()))
+        for k, (x, y) in outs.items():
+            np.testing.assert_array_equal(host(x), host(y), err_msg=k)
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            np.testing.assert_array_equal(host(sa[k]), host(sb[k]), err_msg=k)
+    np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
+    a.check()
+    b.check()
+    assert host(b.stats())[2] > 0
