@@ -1,12 +1,19 @@
 """Throughput benchmark: env-steps/s of the batched CraftWorld on MI355X.
 
-One "step" = one rollout tick of every env on every GPU (craft_step: the
-do_rollout body + step() + satisfies() + the full features() observation,
-auto-reset), i.e. BASELINE.json's metric on 12x12 craft_medium with 65536 envs
-per GPU (configs[2]; configs[3] is the 8-GPU sharding of the same).  Inputs
-(scenario pool, env states) are resident in HBM before the timed region;
-observations stream into a ring of R device buffers (R * 106 MB > the 256 MB
-Infinity Cache) as a trainer's per-tick feature tensors would.
+One "step" = one rollout tick of every env on every GPU: the do_rollout body,
+step(), satisfies() and the full features() observation, with auto-reset.
+This is BASELINE.json's metric on 12x12 craft_medium with 65536 envs per GPU
+(configs[2]); configs[3] is the 8-GPU sharding of the same.
+
+Actions are the hashed random draw (the random-rollout workload), so ticks are
+launched K = 32 at a time through craft_rollout. Every tick still does all of
+its work and writes its full observation, reward, done and success to HBM; the
+envs just stay on chip between ticks. --ticks-per-launch 1 times one craft_step
+launch per tick instead.
+
+Inputs (scenario pool, env states) are resident in HBM before the timed region.
+Observations stream into a ring of R = 16 device buffers (1.7 GB, 6.6x the
+256 MB Infinity Cache), as a trainer's per-tick feature tensors would.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
@@ -40,16 +47,20 @@ def bytes_per_env_step(W, H, window, F):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1000)
-    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--steps", type=int, default=1024)
+    p.add_argument("--warmup", type=int, default=64)
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--world", default="craft_medium_12x12")
     p.add_argument("--pool", type=int, default=1024)
-    p.add_argument("--ring", type=int, default=4, help="observation buffers cycled per tick")
+    p.add_argument("--ring", type=int, default=16,
+                   help="observation buffers cycled per tick (16 x 106 MB: 6.6x the Infinity Cache)")
     p.add_argument("--tile", type=int, default=0, help="envs per workgroup (0 = default)")
-    p.add_argument("--obs-store", type=int, default=1, help="0 write-back, 1 nontemporal, 2 sc1")
-    p.add_argument("--ticks-per-launch", type=int, default=1,
-                   help="K > 1: craft_rollout runs K ticks per launch (same work per tick)")
+    p.add_argument("--obs-store", type=int, default=-1,
+                   help="0 write-back, 1 nontemporal, 2 sc1; -1: the measured best for the path "
+                        "(nontemporal for craft_step, write-back for craft_rollout)")
+    p.add_argument("--ticks-per-launch", type=int, default=32,
+                   help="K > 1: craft_rollout runs K ticks per launch (the same work per tick); "
+                        "1: one craft_step launch per tick")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,13 +100,15 @@ def main():
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
-    sim.tune(args.tile, 0, args.obs_store)
+    K = max(1, args.ticks_per_launch)
+    obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 0)
+    sim.tune(args.tile, 0, obs_store)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
     specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
                             task_ids=tasks)
     sim.reset(*specs)
     F = sim.n_features
-    R, K = args.ring, max(1, args.ticks_per_launch)
+    R = args.ring
     if args.steps % K or args.warmup % K:
         raise SystemExit("--steps and --warmup must be multiples of --ticks-per-launch")
     ring = torch.empty((R, n, F), dtype=sim.obs_dtype, device=dev)     # one tick's obs per slot
@@ -185,7 +198,8 @@ def main():
                        "global_batch": n * world_size, "window": sim.params["WINDOW_WIDTH"],
                        "n_features": F, "obs_dtype": "fp32", "obs_ring": args.ring,
                        "pool": args.pool, "parallelism": f"env-shard x{world_size}",
-                       "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K},
+                       "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
+                       "tile": tile, "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": (f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, {tile}>"

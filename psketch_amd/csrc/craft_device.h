@@ -53,8 +53,31 @@ struct SimView {
 // grid rows [tile][GS] | observation bytes [tile * F] (contiguous rows) |
 // inventory rows [tile][36] | task table [64] u16 | recipes [16][12] |
 // agent words [tile] u32.
+#ifdef CRAFT_STAMPS
+// Diagnostic build only (never the product): thread 0 of every workgroup
+// records s_memrealtime (100 MHz) at phase boundaries into v.stamps[block][8].
+#define STAMP(k)                                                                         \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && v.stamps)                                                    \
+      v.stamps[8 * (int64_t)blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+#define STAMP_END()                                                                      \
+  do {                                                                                   \
+    __syncthreads();                                                                     \
+    if (threadIdx.x == 0 && v.stamps) {                                                  \
+      v.stamps[8 * (int64_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();          \
+      uint32_t xcc;                                                                      \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                 \
+      v.stamps[8 * (int64_t)blockIdx.x + 7] = xcc;                                       \
+    }                                                                                    \
+  } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#define STAMP_END() do {} while (0)
+#endif
+
 struct LdsLayout {
-  int obs, inv, task, rc, agent, bytes;
+  int obs, inv, task, rc, agent, ctrl, bytes;
 };
 __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -64,7 +87,8 @@ __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F) {
   l.task = up16(l.inv + tile * kInvStride);
   l.rc = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.agent = up16(l.rc + CRAFT_MAX_RECIPES * kRecipeBytes);
-  l.bytes = up16(l.agent + tile * 4);
+  l.ctrl = up16(l.agent + tile * 4);         // workgroup-uniform control words (rollout queue)
+  l.bytes = l.ctrl + 16;
   return l;
 }
 
@@ -103,6 +127,9 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   float* reward;           // [ring][n_envs] each, or null
   uint8_t* done;
   int8_t* sat;
+  int32_t chunk;           // ticks per work unit
+  unsigned long long* queue;   // work-unit counter, zeroed before the launch
+  uint32_t* tile_done;     // per tile: chunks completed in this launch, zeroed before the launch
 };
 
 struct Agent {

@@ -89,11 +89,12 @@ __device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t en
 // into the zeroed u8 rows s_obs[TILE][F]: local one-hots, block-max-pooled
 // one-hots, inventory counts, dir one-hot.  s_agent[e] = x | y<<8 | dir<<16 | 1<<24
 // for a live env (0 = skip).
-template <int WIN, int TILE>
+template <int WIN, int TILE, int NTHR = kThreads>
 __device__ __forceinline__ void scatter_features(const SimView& v, const uint8_t* s_grid,
                                                  const uint8_t* s_inv, const uint32_t* s_agent,
                                                  uint8_t* s_obs, int nE, int tid) {
-  constexpr int kParts = kThreads / TILE;        // threads per env
+  constexpr int kParts = NTHR / TILE;            // threads per env
+  static_assert(kParts >= 2, "the scatter needs at least two threads per env");
   const int F = v.F;
   {
     const int e = tid % TILE, part = tid / TILE;

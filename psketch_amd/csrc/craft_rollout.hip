@@ -3,12 +3,28 @@
 // craft_step pays, every tick, for a prologue that moves no observation bytes:
 // the state/inventory/mask loads, the scenario row from L2, the transition and
 // the scatter.  All workgroups of a launch run that prologue together, so HBM
-// idles for its duration (phase stamps).  Here each workgroup keeps
-// its TILE envs on chip for K ticks — state and mask in wave 0's registers, grid
-// rows and inventories in LDS — and loops C -> D -> E with no global
-// synchronisation, so one workgroup's transition and scatter overlap the
-// observation stores of the others on the same CU.  State goes back to HBM once,
-// after the last tick.
+// idles for its duration (phase stamps).  Here a workgroup keeps a
+// tile of envs on chip for a chunk of ticks — state in wave 0's registers, grid
+// rows and inventories in LDS — and software-pipelines the ticks: the transition
+// of tick k+1 (wave 0) runs while the other waves stream tick k's observation.
+//
+// Work distribution.  Workgroups do not stream at equal speed (per-workgroup
+// stamps, tools/rollout_stamps.py: durations from 0.55x to 1x of the launch, odd
+// XCDs slower), so a static tile-per-workgroup launch waits for its slowest
+// workgroups.  The launch is instead cut into units (tile t, chunk c of `chunk`
+// ticks), handed out in chunk-major order from a queue counter; a unit's env
+// state goes back to HBM at its end and the unit (t, c+1) may run on any other
+// workgroup.  That hand-off follows cdna_hip_programming.md Guideline 16 /
+// MI355X_MICROARCH.md (valid forms, plain-store producer): every storing wave
+// drains (s_waitcnt vmcnt(0)), a workgroup barrier, one lane's agent-scope
+// release (which also pushes this unit's observation stores out of the XCD's L2,
+// so a later unit rewriting the same ring slot from another XCD lands last), a
+// second drain, and a relaxed agent-scope store tile_done[t] = c + 1; the
+// consumer wave polls that word relaxed, then one agent-scope acquire, then
+// plain loads.  Queue and flags are zeroed by a memset
+// ahead of every launch.  A unit waits only for its own tile's previous chunk,
+// which was handed out earlier and is held by a running workgroup, so the queue
+// cannot deadlock; spins are bounded anyway.
 //
 // Tick k is exactly craft_step(tick0 + k) with the hashed (or given) actions and
 // writes its outputs to ring slot (tick0 + k) % ring, as a driver cycling craft_step
@@ -18,8 +34,11 @@
 
 namespace craft {
 
-template <int WIN, int TILE>
-__global__ __launch_bounds__(kThreads) void rollout_kernel(SimView v, RolloutArgs a) {
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+// NT threads per workgroup: wave 0 runs the transitions, waves 1.. stream.
+template <int WIN, int TILE, int NT>
+__global__ __launch_bounds__(NT, WIN == 3 ? 4 : 2) void rollout_kernel(SimView v, RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
   uint8_t* s_grid = smem;
@@ -28,25 +47,27 @@ __global__ __launch_bounds__(kThreads) void rollout_kernel(SimView v, RolloutArg
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   uint8_t* s_rc = smem + lay.rc;
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
+  uint32_t* s_ctrl = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
 
+  STAMP(0);
   const int tid = threadIdx.x;
   const int64_t n = v.n_envs;
-  const int64_t env0 = (int64_t)blockIdx.x * TILE;
-  const int nE = (int)min((int64_t)TILE, n - env0);
   const bool want_obs = a.obs != nullptr;
   const int F = v.F;
   const int esz = v.obs_fmt == CRAFT_OBS_F32 ? 4 : (v.obs_fmt == CRAFT_OBS_BF16 ? 2 : 1);
+  const int n_tiles = (int)((n + TILE - 1) / TILE);
+  const int n_chunks = (a.n_ticks + a.chunk - 1) / a.chunk;
+  const uint32_t n_units = (uint32_t)n_tiles * (uint32_t)n_chunks;
 
-  // ---- A (once): wave 0 loads its envs -------------------------------------------------------
-  // Loop-carried per lane: the packed state word and the init word only.  The
-  // cleared-cell mask is not carried: cells are only ever cleared, so this
-  // episode's mask is exactly {c : pool[c] != 0 and grid[c] == 0} and is rebuilt
-  // from the LDS row when the state goes back to HBM.
+  // Per lane of wave 0, for the current unit: the packed state word and the init
+  // word.  The cleared-cell mask is not carried: cells are only ever cleared, so
+  // this episode's mask is exactly {c : pool[c] != 0 and grid[c] == 0} and is
+  // rebuilt from the LDS row when the state goes back to HBM.
   Agent s{};
   uint64_t st = 0;
   uint32_t init_word = 0;
   bool live = false;
-  const int64_t slot = env0 + tid;
+  int64_t slot = 0;
   uint8_t* g = s_grid + tid * v.GS;
   uint8_t* iv = s_inv + tid * kInvStride;
   uint32_t* ivw = reinterpret_cast<uint32_t*>(iv);
@@ -71,42 +92,6 @@ __global__ __launch_bounds__(kThreads) void rollout_kernel(SimView v, RolloutArg
         }
     }
   };
-  if (tid < TILE) {
-    for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
-    for (int t = tid; t < CRAFT_MAX_RECIPES * kRecipeBytes / 4; t += TILE)
-      reinterpret_cast<uint32_t*>(s_rc)[t] = reinterpret_cast<const uint32_t*>(v.rc)[t];
-    live = tid < nE;
-    uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (live) {
-      st = v.state[slot];
-      init_word = v.init[slot];
-      const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
-      const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
-      ivw[0] = i0.x; ivw[1] = i0.y; ivw[2] = i0.z; ivw[3] = i0.w;
-      ivw[4] = i1.x; ivw[5] = i1.y; ivw[6] = i1.z; ivw[7] = i1.w;
-      m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
-      m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
-      s = unpack_state(st);
-      if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
-        latch_error(v.err, CRAFT_EINVAL, slot);   // never initialised by reset / set_state
-        live = false;
-      }
-    }
-    if (live) {
-      load_row();
-#pragma unroll
-      for (int w = 0; w < 8; ++w) {                         // cells cleared this episode
-        uint32_t mm = m[w];
-        while (mm) {
-          g[w * 32 + __ffs(mm) - 1] = 0;
-          mm &= mm - 1;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
 
   // ---- C: the do_rollout tick of wave 0's envs (trainers/imitation.py:59-73) ------------------
   auto tick_c = [&](int k) {
@@ -170,44 +155,111 @@ __global__ __launch_bounds__(kThreads) void rollout_kernel(SimView v, RolloutArg
     n_step += (uint32_t)__popcll(bt);
   };
 
-  // Software pipeline, two barriers per tick: after the scatter D(k), wave 0 runs
-  // the transition C(k+1) while waves 1-3 stream E(k) and clear the rows they
-  // read, so the latency-bound transition hides under the observation stores.
+  // ---- once per workgroup: static tables, cleared observation rows ------------------------------
   if (tid < TILE) {
-    if (a.n_ticks > 0) tick_c(0);
-  } else if (want_obs && tid >= 64) {
-    uint4* z = reinterpret_cast<uint4*>(s_obs);
-    const int n16 = (nE * F + 15) >> 4;
-    for (int i = tid - 64; i < n16; i += kThreads - 64) z[i] = make_uint4(0, 0, 0, 0);
+    for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
+    for (int t = tid; t < CRAFT_MAX_RECIPES * kRecipeBytes / 4; t += TILE)
+      reinterpret_cast<uint32_t*>(s_rc)[t] = reinterpret_cast<const uint32_t*>(v.rc)[t];
   }
-  for (int k = 0; k < a.n_ticks; ++k) {
-    if (!want_obs) {                 // workgroup-uniform: wave 0 alone runs the ticks
-      if (tid < TILE && k + 1 < a.n_ticks) tick_c(k + 1);
-      continue;
-    }
-    __syncthreads();                 // C(k) and the cleared rows are visible
-    scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
-    __syncthreads();                 // rows complete; C(k+1) may now change grids and agents
-    if (tid < 64) {
-      if (tid < TILE && k + 1 < a.n_ticks) tick_c(k + 1);
-    } else {
-      const int64_t r = (a.tick0 + k) % a.ring;
-      void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
-      const int et = tid - 64;
-      switch (v.obs_fmt) {
-        case CRAFT_OBS_BF16:
-          stream_obs<CRAFT_OBS_BF16, kThreads - 64, true>(s_obs, out, env0, F, nE, v.obs_policy, et); break;
-        case CRAFT_OBS_U8:
-          stream_obs<CRAFT_OBS_U8, kThreads - 64, true>(s_obs, out, env0, F, nE, v.obs_policy, et); break;
-        default:
-          stream_obs<CRAFT_OBS_F32, kThreads - 64, true>(s_obs, out, env0, F, nE, v.obs_policy, et); break;
-      }
-    }
+  if (want_obs) {
+    uint4* z = reinterpret_cast<uint4*>(s_obs);
+    const int n16 = (TILE * F + 15) >> 4;
+    for (int i = tid; i < n16; i += NT) z[i] = make_uint4(0, 0, 0, 0);
   }
 
-  // ---- write back (once) -------------------------------------------------------------------------
-  if (tid < TILE) {
-    if (live) {
+  for (;;) {
+    // ---- next unit ------------------------------------------------------------------------------
+    if (tid == 0) s_ctrl[0] = (uint32_t)atomicAdd(a.queue, 1ull);
+    __syncthreads();
+    const uint32_t u = s_ctrl[0];
+    if (u >= n_units) break;                            // workgroup-uniform exit
+    const int t = (int)(u % (uint32_t)n_tiles), c = (int)(u / (uint32_t)n_tiles);
+    const int k0 = c * a.chunk, k1 = min(a.n_ticks, k0 + a.chunk);
+    const int64_t env0 = (int64_t)t * TILE;
+    const int nE = (int)min((int64_t)TILE, n - env0);
+
+    // ---- A: wave 0 takes over the tile (after the tile's previous chunk is published) -----------
+    if (tid < 64) {
+      if (c > 0) {
+        bool ok = true;
+        if (tid == 0) {                                 // ONE lane polls ONE word, relaxed
+          const gu32* f = (const gu32*)(a.tile_done + t);
+          for (uint32_t spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)c;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 26)) { ok = false; break; }   // bounded: never hang the GPU
+          }
+          if (!ok) latch_error(v.err, CRAFT_EINVARIANT, env0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // after the match: drop stale L1 lines
+      }
+      if (tid < TILE) {
+        slot = env0 + tid;
+        live = tid < nE;
+        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (live) {
+          st = v.state[slot];
+          init_word = v.init[slot];
+          const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
+          const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+          ivw[0] = i0.x; ivw[1] = i0.y; ivw[2] = i0.z; ivw[3] = i0.w;
+          ivw[4] = i1.x; ivw[5] = i1.y; ivw[6] = i1.z; ivw[7] = i1.w;
+          m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
+          m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
+          s = unpack_state(st);
+          if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
+            latch_error(v.err, CRAFT_EINVAL, slot);     // never initialised by reset / set_state
+            live = false;
+          }
+        }
+        if (live) {
+          load_row();
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {                 // cells cleared this episode
+            uint32_t mm = m[w];
+            while (mm) {
+              g[w * 32 + __ffs(mm) - 1] = 0;
+              mm &= mm - 1;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        tick_c(k0);
+      }
+    }
+
+    // ---- software pipeline, two barriers per tick: after the scatter D(k), wave 0 runs the
+    // transition C(k+1) while the other waves stream E(k) and clear the rows they read --------
+    for (int k = k0; k < k1; ++k) {
+      if (!want_obs) {                                  // workgroup-uniform: wave 0 alone
+        if (tid < TILE && k + 1 < k1) tick_c(k + 1);
+        continue;
+      }
+      __syncthreads();                                  // C(k) and the cleared rows are visible
+      scatter_features<WIN, TILE, NT>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
+      __syncthreads();                                  // rows complete; C(k+1) may change grids
+      if (tid < 64) {
+        if (tid < TILE && k + 1 < k1) tick_c(k + 1);
+      } else {
+        const int64_t r = (a.tick0 + k) % a.ring;
+        void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
+        const int et = tid - 64;
+        switch (v.obs_fmt) {
+          case CRAFT_OBS_BF16:
+            stream_obs<CRAFT_OBS_BF16, NT - 64, true>(s_obs, out, env0, F, nE, v.obs_policy, et); break;
+          case CRAFT_OBS_U8:
+            stream_obs<CRAFT_OBS_U8, NT - 64, true>(s_obs, out, env0, F, nE, v.obs_policy, et); break;
+          default:
+            stream_obs<CRAFT_OBS_F32, NT - 64, true>(s_obs, out, env0, F, nE, v.obs_policy, et); break;
+        }
+      }
+    }
+
+    // ---- publish the tile for the unit (t, c + 1): its state, and every output this unit wrote ----
+    // (a later unit may rewrite the same ring slots from another XCD, so the release must cover
+    // the observation stores of all waves, not only the state)
+    if (tid < TILE && live) {
       v.state[slot] = st;
       v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
       v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
@@ -216,10 +268,10 @@ __global__ __launch_bounds__(kThreads) void rollout_kernel(SimView v, RolloutArg
       const uint32_t* cur = reinterpret_cast<const uint32_t*>(g);
       uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int q = 0; q < (v.CS >> 2); ++q) {
-        const uint32_t p = row[q], c = cur[q];
+        const uint32_t p = row[q], cc = cur[q];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const bool cleared = ((p >> (8 * b)) & 0xffu) != 0 && ((c >> (8 * b)) & 0xffu) == 0;
+          const bool cleared = ((p >> (8 * b)) & 0xffu) != 0 && ((cc >> (8 * b)) & 0xffu) == 0;
           const int cell = 4 * q + b;
           if (cleared) m[cell >> 5] |= 1u << (cell & 31);
         }
@@ -227,12 +279,25 @@ __global__ __launch_bounds__(kThreads) void rollout_kernel(SimView v, RolloutArg
       v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
       v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
     }
-    if (tid == 0) {
-      unsigned long long* srow = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
-      atomicAdd(srow + 0, (unsigned long long)n_succ);
-      atomicAdd(srow + 1, (unsigned long long)n_end);
-      atomicAdd(srow + 2, (unsigned long long)n_step);
+    if (c + 1 < n_chunks) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // write back this XCD's dirty L2 lines
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // keep: the compiler may drop the fence's own
+        __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    __syncthreads();                                    // s_ctrl and the LDS rows are reused
+  }
+
+  STAMP_END();
+  if (tid == 0) {
+    unsigned long long* srow = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
+    atomicAdd(srow + 0, (unsigned long long)n_succ);
+    atomicAdd(srow + 1, (unsigned long long)n_end);
+    atomicAdd(srow + 2, (unsigned long long)n_step);
   }
 }
 
@@ -240,7 +305,10 @@ template <int WIN, int TILE>
 static hipError_t launch_rollout_one(const SimView& v, const RolloutArgs& a, size_t lds, hipStream_t st) {
   const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
   if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
-  hipLaunchKernelGGL((rollout_kernel<WIN, TILE>), dim3((unsigned)tiles), dim3(kThreads), lds, st, v, a);
+  constexpr int NT = TILE == 64 ? 256 : 128;
+  // persistent workgroups: at most what the chip holds (8 per CU), never more than the tiles
+  const int64_t grid = tiles < 8 * 256 ? tiles : 8 * 256;
+  hipLaunchKernelGGL((rollout_kernel<WIN, TILE, NT>), dim3((unsigned)grid), dim3(NT), lds, st, v, a);
   return hipGetLastError();
 }
 

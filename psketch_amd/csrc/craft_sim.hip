@@ -137,6 +137,9 @@ struct craft_sim {
   SimView view{};
   int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
   int resident_cap = 0;             // 0: no cap on tile workgroups per CU
+  int rollout_chunk = 0;            // craft_rollout ticks per work unit (0: the whole launch)
+  uint8_t* d_sync = nullptr;        // craft_rollout: work-unit counter + per-tile chunk flags
+  size_t sync_bytes = 0;
   std::string last_error;
 };
 
@@ -306,6 +309,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_rc, rcb.size());
   ALLOC(s->d_stats, 4 * sizeof(int64_t) * s->n_tiles);
   ALLOC(s->d_err, 4 * sizeof(int32_t));
+  s->sync_bytes = (16 + 4 * (size_t)((n_envs + 15) / 16) + 15) & ~size_t(15);   // queue + tile_done
+  ALLOC(s->d_sync, s->sync_bytes);
 #undef ALLOC
   if ((e = hipMemcpy(s->d_task, task_tab.data(), sizeof(uint16_t) * task_tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "task table");
@@ -361,6 +366,14 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
   return CRAFT_OK;
 }
 
+int craft_sim_tune_rollout(craft_sim_t* s, int32_t chunk_ticks) {
+  if (!s) return CRAFT_EINVAL;
+  if (chunk_ticks < 0 || chunk_ticks > 4096)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_rollout: chunk_ticks must be 0..4096");
+  s->rollout_chunk = chunk_ticks;
+  return CRAFT_OK;
+}
+
 int craft_sim_set_obs_format(craft_sim_t* s, int32_t format) {
   if (!s) return CRAFT_EINVAL;
   if (format != CRAFT_OBS_F32 && format != CRAFT_OBS_BF16 && format != CRAFT_OBS_U8)
@@ -382,6 +395,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_rc);
   (void)hipFree(s->d_stats);
   (void)hipFree(s->d_err);
+  (void)hipFree(s->d_sync);
   delete s;
   return CRAFT_OK;
 }
@@ -508,6 +522,11 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   a.reward = reward;
   a.done = done;
   a.sat = success;
+  a.chunk = s->rollout_chunk > 0 ? s->rollout_chunk : (n_ticks > 0 ? n_ticks : 1);
+  a.queue = reinterpret_cast<unsigned long long*>(s->d_sync);
+  a.tile_done = reinterpret_cast<uint32_t*>(s->d_sync + 16);
+  if (n_ticks > 0)
+    HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
   hipError_t e = craft::launch_rollout(s->cfg.window_width, s->tile, s->view, a, lds_bytes(s, s->tile),
                                        reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");

@@ -20,28 +20,6 @@
 
 namespace craft {
 
-#ifdef CRAFT_STAMPS
-// Diagnostic build only (never the product): thread 0 of every workgroup
-// records s_memrealtime (100 MHz) at phase boundaries into v.stamps[block][8].
-#define STAMP(k)                                                                         \
-  do {                                                                                   \
-    if (threadIdx.x == 0 && v.stamps)                                                    \
-      v.stamps[8 * (int64_t)blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();        \
-  } while (0)
-#define STAMP_END()                                                                      \
-  do {                                                                                   \
-    __syncthreads();                                                                     \
-    if (threadIdx.x == 0 && v.stamps) {                                                  \
-      v.stamps[8 * (int64_t)blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();          \
-      uint32_t xcc;                                                                      \
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));                 \
-      v.stamps[8 * (int64_t)blockIdx.x + 7] = xcc;                                       \
-    }                                                                                    \
-  } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#define STAMP_END() do {} while (0)
-#endif
 
 template <int WIN, int MODE, int TILE>
 __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {

@@ -381,17 +381,21 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
     sim.check()
 
 
-@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given", [
-    ("craft_medium_12x12", 12, 0, "f32", True, False),
-    ("craft_medium_12x12", 12, 16, "bf16", True, True),
-    ("craft_medium_12x12", 12, 32, "u8", False, True),
-    ("craft_medium_12x12_w5", 12, 0, "f32", True, False),
-    ("craft_16x16_w7", 16, 0, "f32", False, False),
-    ("craft_medium", 8, 64, "f32", True, True)])
-def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given):
+@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given,chunk", [
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 0),
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 1),
+    ("craft_medium_12x12", 12, 16, "bf16", True, True, 2),
+    ("craft_medium_12x12", 12, 32, "u8", False, True, 3),
+    ("craft_medium_12x12_w5", 12, 0, "f32", True, False, 2),
+    ("craft_16x16_w7", 16, 0, "f32", False, False, 0),
+    ("craft_medium", 8, 64, "f32", True, True, 1)])
+def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, chunk):
     """craft_rollout(K ticks) == K craft_step calls: observation / reward / done /
     success rings, final states and episode statistics, bit for bit; several
-    launches in a row (state written back and picked up again)."""
+    launches in a row (state written back and picked up again).  Small work
+    units (chunk) hand each tile between workgroups several times per launch,
+    and the ring (3) is shorter than a launch, so slots are rewritten by later
+    units that may run on another XCD."""
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 64)
     n = 5000                                   # a partial last tile
@@ -404,6 +408,7 @@ def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given):
     for _ in range(2):
         sim = sim_with_pool(world, n, pool)
         sim.tune(tile, 0, 1)
+        sim.tune_rollout(chunk)
         sim.set_obs_format(fmt)
         sim.reset(*specs)
         sims.append(sim)

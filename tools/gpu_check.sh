@@ -24,7 +24,7 @@ rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"; [ $
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-      python "$REPO/bench.py" --steps 500 --warmup 20 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+      python "$REPO/bench.py" --steps 512 --warmup 64 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.err"; [ $rc -eq 0 ] || exit $rc
   find "$OUT/prof" -name '*stats*' | head
 fi

@@ -19,7 +19,7 @@ def main():
     sim = CraftSim("craft_medium_12x12", n_envs=n, device=0, pool_capacity=1024)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, 1024)
     sim.load_pool(grids)
-    sim.tune(64, 0, 0)
+    sim.tune(int(sys.argv[2]) if len(sys.argv) > 2 else 64, 0, int(sys.argv[3]) if len(sys.argv) > 3 else 0)
     sim.reset(*synthetic_specs(grids, 12, 12, n, task_ids=[t.id for t in sim.task_manager.dataset_tasks()]))
     keep = []
     tick = 0
