@@ -299,6 +299,21 @@ int craft_get_state(craft_sim_t* sim, const int32_t* slots, int64_t n, int32_t* 
 int craft_set_state(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* spec,
                     const int32_t* agent, const int32_t* inventory, void* stream);
 
+/* make_data.sample_scenario (make_data.py:105-144) on the GPU, straight into pool
+ * rows [first, first + count): boundary ring, n_per_primitive of each primitive,
+ * then the workshops, each placed by random_free with its connectivity checks,
+ * then the initial position (init_pos_out: device int32[count][2], may be NULL).
+ * Scenario s draws from its own splitmix64 stream keyed by seed and its global
+ * id scenario_id0 + s (numpy's sequential MT19937 stream cannot be split across
+ * lanes), so results do not depend on how ids are sharded; otherwise the
+ * algorithm and acceptance tests are make_data.py's.  No de-duplication.  Where
+ * a placement finds no valid cell in 2^20 draws, CRAFT_EINVARIANT latches. */
+int craft_pool_generate(craft_sim_t* sim, uint64_t seed, int64_t scenario_id0, int32_t first,
+                        int32_t count, int32_t boundary_kind, const int32_t* primitives,
+                        int32_t n_primitive_kinds, int32_t n_per_primitive,
+                        const int32_t* workshop_kind, int32_t n_workshops, int32_t* init_pos_out,
+                        void* stream);
+
 /* ---- host-side scenario generation ------------------------------------------ */
 
 /* make_data.sample_scenario (make_data.py:105-144) with `random_free`

@@ -303,3 +303,166 @@ int64_t oracle_bench(const craft_config_t* cfg, const uint8_t* pool, oracle_env_
 }
 
 int oracle_sizeof_config(void) { return (int)sizeof(craft_config_t); }
+
+/* ---- scenario generation (make_data.py:27-144) ------------------------------------------ */
+
+typedef struct {
+  int kind;               /* 0 splitmix64 per scenario, 1 numpy legacy MT19937 */
+  uint64_t sm;
+  uint32_t mt[624];
+  int mti;
+} gen_rng_t;
+
+static void mt_seed(gen_rng_t* r, uint32_t s) {         /* init_genrand, as RandomState(int) */
+  r->mt[0] = s;
+  for (int i = 1; i < 624; ++i) r->mt[i] = 1812433253u * (r->mt[i - 1] ^ (r->mt[i - 1] >> 30)) + (uint32_t)i;
+  r->mti = 624;
+}
+
+static uint32_t mt_next(gen_rng_t* r) {
+  if (r->mti >= 624) {
+    for (int i = 0; i < 624; ++i) {
+      const uint32_t y = (r->mt[i] & 0x80000000u) | (r->mt[(i + 1) % 624] & 0x7fffffffu);
+      r->mt[i] = r->mt[(i + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    r->mti = 0;
+  }
+  uint32_t y = r->mt[r->mti++];
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+static uint32_t sm_next32(gen_rng_t* r) {                /* the splitmix64 sequence, high half */
+  r->sm += 0x9E3779B97F4A7C15ull;
+  uint64_t z = r->sm;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((z ^ (z >> 31)) >> 32);
+}
+
+/* random.randint(n) */
+static int gen_randint(gen_rng_t* r, int n) {
+  if (r->kind == 1) {                                    /* numpy legacy: masked rejection */
+    const uint32_t max = (uint32_t)(n - 1);
+    if (max == 0) return 0;
+    uint32_t mask = max;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    while ((v = mt_next(r) & mask) > max) {}
+    return (int)v;
+  }
+  uint64_t m = (uint64_t)sm_next32(r) * (uint32_t)n;     /* Lemire: unbiased multiply-shift */
+  uint32_t l = (uint32_t)m;
+  if (l < (uint32_t)n) {
+    const uint32_t t = (uint32_t)(-(uint32_t)n) % (uint32_t)n;
+    while (l < t) {
+      m = (uint64_t)sm_next32(r) * (uint32_t)n;
+      l = (uint32_t)m;
+    }
+  }
+  return (int)(m >> 32);
+}
+
+/* all_free_cells_reachable (make_data.py:27-72): FIFO BFS from init (or the first free cell,
+ * x-major), moves into occupied cells blocked; every free cell reached? */
+static int all_free_cells_reachable(const uint8_t* nav, int W, int H, int ix, int iy) {
+  uint8_t seen[CRAFT_MAX_CELLS];
+  int queue[1000];
+  if (ix < 0) {
+    for (int c = 0; c < W * H && ix < 0; ++c)
+      if (!nav[c]) { ix = c / H; iy = c % H; }
+  }
+  memset(seen, 0, sizeof(seen));
+  int start = 0, end = 0;
+  queue[end++] = ix * H + iy;
+  seen[ix * H + iy] = 1;
+  while (start < end) {
+    const int p = queue[start++];
+    const int x = p / H, y = p % H;
+    for (int a = 0; a < 4; ++a) {
+      int nx = x + DX[a], ny = y + DY[a];
+      if (nav[nx * H + ny]) { nx = x; ny = y; }
+      const int q = nx * H + ny;
+      if (!seen[q]) { seen[q] = 1; queue[end++] = q; }
+    }
+  }
+  for (int c = 0; c < W * H; ++c)
+    if (!nav[c] && !seen[c]) return 0;
+  return 1;
+}
+
+/* random_free (make_data.py:74-103), keep_connected=True; nav is the occupancy image. */
+static int random_free(gen_rng_t* r, uint8_t* nav, int W, int H, int* ox, int* oy) {
+  for (int draws = 0; draws < (1 << 20); ++draws) {
+    const int x = gen_randint(r, W), y = gen_randint(r, H);
+    if (nav[x * H + y]) continue;
+    nav[x * H + y] = 1;
+    int good = all_free_cells_reachable(nav, W, H, -1, -1);
+    for (int i = 0; good && i < W; ++i)
+      for (int j = 0; good && j < H; ++j)
+        if (nav[i * H + j] && 0 < i && i < W - 1 && 0 < j && j < H - 1 &&
+            !all_free_cells_reachable(nav, W, H, i, j))
+          good = 0;
+    nav[x * H + y] = 0;
+    if (good) { *ox = x; *oy = y; return 0; }
+  }
+  return -1;
+}
+
+static int sample_scenario(gen_rng_t* r, int W, int H, int boundary, const int32_t* prims, int n_prim,
+                           int n_per, const int32_t* ws, int n_ws, uint8_t* grid, int32_t* init) {
+  memset(grid, 0, (size_t)W * H);
+  for (int x = 0; x < W; ++x)
+    for (int y = 0; y < H; ++y)
+      if (x == 0 || y == 0 || x == W - 1 || y == H - 1) grid[x * H + y] = (uint8_t)boundary;
+  uint8_t nav[CRAFT_MAX_CELLS];
+  int x, y;
+  for (int c = 0; c < W * H; ++c) nav[c] = grid[c] != 0;
+  for (int p = 0; p < n_prim; ++p)                                 /* ingredients */
+    for (int i = 0; i < n_per; ++i) {
+      if (random_free(r, nav, W, H, &x, &y)) return -1;
+      grid[x * H + y] = (uint8_t)prims[p];
+      nav[x * H + y] = 1;
+    }
+  for (int i = 0; i < n_ws; ++i) {                                 /* crafting stations */
+    if (random_free(r, nav, W, H, &x, &y)) return -1;
+    grid[x * H + y] = (uint8_t)ws[i];
+    nav[x * H + y] = 1;
+  }
+  if (random_free(r, nav, W, H, &x, &y)) return -1;               /* init pos */
+  init[0] = x;
+  init[1] = y;
+  return 0;
+}
+
+int oracle_generate_scenarios(int32_t W, int32_t H, int32_t boundary, const int32_t* prims,
+                              int32_t n_prim, int32_t n_per, const int32_t* ws, int32_t n_ws,
+                              int32_t rng_kind, uint64_t seed, int64_t id0, int32_t count,
+                              int32_t dedup, uint8_t* grids_out, int32_t* init_out,
+                              uint32_t* mt_state_out) {
+  const int C = W * H;
+  gen_rng_t r;
+  memset(&r, 0, sizeof(r));
+  r.kind = rng_kind;
+  if (rng_kind == 1) mt_seed(&r, (uint32_t)seed);
+  for (int s = 0; s < count; ++s) {
+    uint8_t* g = grids_out + (size_t)s * C;
+    if (rng_kind == 0) r.sm = seed ^ ((uint64_t)(id0 + s) * 0xD1B54A32D192ED03ull);
+    for (;;) {
+      if (sample_scenario(&r, W, H, boundary, prims, n_prim, n_per, ws, n_ws, g, init_out + 2 * s))
+        return -1;
+      int dup = 0;
+      for (int t = 0; dedup && rng_kind == 1 && t < s && !dup; ++t)
+        dup = memcmp(g, grids_out + (size_t)t * C, (size_t)C) == 0;
+      if (!dup) break;
+    }
+  }
+  if (mt_state_out && rng_kind == 1) {
+    memcpy(mt_state_out, r.mt, sizeof(r.mt));
+    mt_state_out[624] = (uint32_t)r.mti;
+  }
+  return 0;
+}

@@ -77,6 +77,24 @@ int oracle_batch_tick(const craft_config_t* cfg, const uint8_t* pool, oracle_env
 int64_t oracle_bench(const craft_config_t* cfg, const uint8_t* pool, oracle_env_t* envs,
                      int64_t n, int64_t ticks, uint64_t seed, float* scratch_row);
 
+/* make_data.sample_scenario (make_data.py:105-144) with random_free
+ * (make_data.py:74-103) and all_free_cells_reachable (make_data.py:27-72),
+ * literally (one FIFO BFS per connectivity check), for `count` scenarios.
+ * rng_kind 1: ONE stream, numpy's legacy RandomState(seed) (MT19937,
+ *   init_genrand; randint by masked rejection), scenarios drawn in order and, with
+ *   dedup, redrawn while equal to an earlier one (make_data.py:166-178);
+ *   mt_state_out (625 words: key[624], pos) receives the final state.
+ * rng_kind 0: one splitmix64 stream per scenario, keyed by its global id
+ *   (scenario_id0 + s): the stream of craft_pool_generate (include/craft.h).
+ * grids_out: uint8[count][W*H] kind ids, x-major; init_out: int32[count][2].
+ * Returns 0, or -1 if a placement found no valid cell in 2^20 draws. */
+int oracle_generate_scenarios(int32_t width, int32_t height, int32_t boundary_kind,
+                              const int32_t* primitives, int32_t n_primitive_kinds,
+                              int32_t n_per_primitive, const int32_t* workshop_kind,
+                              int32_t n_workshops, int32_t rng_kind, uint64_t seed,
+                              int64_t scenario_id0, int32_t count, int32_t dedup,
+                              uint8_t* grids_out, int32_t* init_out, uint32_t* mt_state_out);
+
 #ifdef __cplusplus
 }
 #endif

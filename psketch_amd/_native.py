@@ -110,6 +110,8 @@ SIGNATURES = {
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32]),
     "craft_pool_load": (_i32, [_vp, _vp, _i32, _i32]),
+    "craft_pool_generate": (_i32, [_vp, _u64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32,
+                                   _vp, _vp]),
     "craft_reset": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "craft_step": (_i32, [_vp, _vp, _u64, _i64, _u32, _vp, _vp, _vp, _vp, _vp]),
     "craft_step_ex": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp]),

@@ -132,6 +132,18 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   uint32_t* tile_done;     // per tile: chunks completed in this launch, zeroed before the launch
 };
 
+struct ScenarioArgs {      // craft_pool_generate
+  uint64_t seed;
+  int64_t id0;             // global id of scenario 0 of this launch
+  int32_t count;
+  int32_t first;           // pool row of scenario 0
+  int32_t boundary;
+  int32_t n_prim, n_per, n_ws;
+  int32_t prim[8];
+  int32_t ws[8];
+  int32_t* init_out;       // [count][2] or null
+};
+
 struct Agent {
   int x, y, dir, frozen, timer, scen, task;
 };

@@ -1,7 +1,7 @@
 // craft_sim.hip — host side of the C ABI (include/craft.h): handle lifetime,
 // scenario pool, launches, state I/O and episode statistics.
 // Kernels: craft_tile.hip (tick / transition / observe / reset), craft_rollout.hip
-// (multi-tick), craft_teacher.hip.
+// (multi-tick), craft_teacher.hip, craft_scenarios.hip (pool generation).
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -16,6 +16,7 @@ hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const 
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st);
 hipError_t launch_rollout(int win, int tile, const SimView& v, const RolloutArgs& a, size_t lds,
                           hipStream_t st);
+hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t st);
 
 namespace {
 
@@ -447,6 +448,43 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
   HIP_TRY(s, hipSetDevice(s->device));
   if (count)
     HIP_TRY(s, hipMemcpy(s->d_pool + (size_t)first * CS, staged.data(), staged.size(), hipMemcpyHostToDevice));
+  if (first + count > s->pool_count) s->pool_count = first + count;
+  s->view.pool_count = s->pool_count;
+  return CRAFT_OK;
+}
+
+int craft_pool_generate(craft_sim_t* s, uint64_t seed, int64_t scenario_id0, int32_t first, int32_t count,
+                        int32_t boundary_kind, const int32_t* primitives, int32_t n_primitive_kinds,
+                        int32_t n_per_primitive, const int32_t* workshop_kind, int32_t n_workshops,
+                        int32_t* init_pos_out, void* stream) {
+  if (!s || first < 0 || count < 0 || n_primitive_kinds < 0 || n_primitive_kinds > 8 || n_per_primitive < 0 ||
+      n_workshops < 0 || n_workshops > 8 || (n_primitive_kinds && !primitives) || (n_workshops && !workshop_kind))
+    return fail(s, CRAFT_EINVAL, "craft_pool_generate: bad argument");
+  if ((int64_t)first + count > s->pool_capacity) return fail(s, CRAFT_ERANGE, "craft_pool_generate: beyond pool capacity");
+  const int K = s->cfg.n_kinds, W = s->cfg.width, H = s->cfg.height;
+  auto bad_kind = [&](int k) { return k <= 0 || k >= K; };
+  if (bad_kind(boundary_kind)) return fail(s, CRAFT_EINVAL, "craft_pool_generate: bad boundary kind");
+  for (int i = 0; i < n_primitive_kinds; ++i)
+    if (bad_kind(primitives[i])) return fail(s, CRAFT_EINVAL, "craft_pool_generate: bad primitive kind");
+  for (int i = 0; i < n_workshops; ++i)
+    if (bad_kind(workshop_kind[i])) return fail(s, CRAFT_EINVAL, "craft_pool_generate: bad workshop kind");
+  if ((int64_t)n_primitive_kinds * n_per_primitive + n_workshops + 1 > (int64_t)(W - 2) * (H - 2))
+    return fail(s, CRAFT_EINVAL, "craft_pool_generate: more objects than interior cells");
+  craft::ScenarioArgs a{};
+  a.seed = seed;
+  a.id0 = scenario_id0;
+  a.count = count;
+  a.first = first;
+  a.boundary = boundary_kind;
+  a.n_prim = n_primitive_kinds;
+  a.n_per = n_per_primitive;
+  a.n_ws = n_workshops;
+  for (int i = 0; i < n_primitive_kinds; ++i) a.prim[i] = primitives[i];
+  for (int i = 0; i < n_workshops; ++i) a.ws[i] = workshop_kind[i];
+  a.init_out = init_pos_out;
+  HIP_TRY(s, hipSetDevice(s->device));
+  hipError_t e = craft::launch_scenarios(s->view, a, reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(s, e, "craft_pool_generate launch");
   if (first + count > s->pool_count) s->pool_count = first + count;
   s->view.pool_count = s->pool_count;
   return CRAFT_OK;

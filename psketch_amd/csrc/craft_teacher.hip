@@ -1,98 +1,9 @@
 // craft_teacher.hip — DemonstrationTeacher on the GPU: the hint-tree walk of
 // BaseTeacher.find_incomplete_subtask and find_closest_resources' BFS, one lane
 // per env, the BFS held as per-direction position bitsets in registers.
-#include "craft_device.h"
+#include "craft_bits.h"
 
 namespace craft {
-
-// A set of cells as NW 32-bit words (cell c = bit c & 31 of word c >> 5).
-// Multi-word shifts use v_alignbit_b32 (one funnel shift per word).
-template <int NW>
-struct Bits {
-  uint32_t w[NW];
-};
-
-template <int NW>
-__device__ __forceinline__ Bits<NW> bzero() {
-  Bits<NW> r;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = 0u;
-  return r;
-}
-template <int NW>
-__device__ __forceinline__ Bits<NW> band(const Bits<NW>& a, const Bits<NW>& b) {
-  Bits<NW> r;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] & b.w[i];
-  return r;
-}
-template <int NW>
-__device__ __forceinline__ Bits<NW> bor(const Bits<NW>& a, const Bits<NW>& b) {
-  Bits<NW> r;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] | b.w[i];
-  return r;
-}
-template <int NW>
-__device__ __forceinline__ Bits<NW> bandn(const Bits<NW>& a, const Bits<NW>& b) {
-  Bits<NW> r;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = a.w[i] & ~b.w[i];
-  return r;
-}
-template <int NW>
-__device__ __forceinline__ bool bany(const Bits<NW>& a) {
-  uint32_t x = 0;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) x |= a.w[i];
-  return x != 0u;
-}
-template <int NW>
-__device__ __forceinline__ bool btest(const Bits<NW>& a, int p) {
-  uint32_t x = 0;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) x |= (i == (p >> 5)) ? a.w[i] : 0u;
-  return (x >> (p & 31)) & 1u;
-}
-template <int NW>
-__device__ __forceinline__ Bits<NW> bbit(int p) {
-  Bits<NW> r;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) r.w[i] = (i == (p >> 5)) ? (1u << (p & 31)) : 0u;
-  return r;
-}
-template <int NW>
-__device__ __forceinline__ int blowest(const Bits<NW>& a) {   // INT_MAX if empty
-  int r = INT_MAX;
-#pragma unroll
-  for (int i = NW - 1; i >= 0; --i)
-    if (a.w[i]) r = i * 32 + __ffs(a.w[i]) - 1;
-  return r;
-}
-template <int NW>
-__device__ __forceinline__ int bhighest(const Bits<NW>& a) {  // -1 if empty
-  int r = -1;
-#pragma unroll
-  for (int i = 0; i < NW; ++i)
-    if (a.w[i]) r = i * 32 + 31 - __clz(a.w[i]);
-  return r;
-}
-// p -> p + d for every member (0 < |d| < 32); members shifted past either end drop out.
-template <int NW>
-__device__ __forceinline__ Bits<NW> bshift(const Bits<NW>& a, int d) {
-  Bits<NW> r;
-  if (d > 0) {
-    r.w[0] = a.w[0] << d;
-#pragma unroll
-    for (int i = 1; i < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i], a.w[i - 1], 32 - d);
-  } else {
-    const int s = -d;
-#pragma unroll
-    for (int i = 0; i + 1 < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i + 1], a.w[i], s);
-    r.w[NW - 1] = a.w[NW - 1] >> s;
-  }
-  return r;
-}
 
 // find_closest_resources (teachers/base.py:27-34) over shortest_path
 // (teachers/base.py:36-87) as ONE level-synchronous BFS over (pos, dir) states

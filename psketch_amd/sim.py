@@ -145,6 +145,25 @@ class CraftSim:
         self.load_pool(grids)
         return grids, init_pos
 
+    def generate_pool(self, count, seed=0, first=0, scenario_id0=None, init_pos=False):
+        """make_data.sample_scenario x count on the GPU, straight into pool rows
+        [first, first + count) (include/craft.h craft_pool_generate); scenario s
+        draws from a stream keyed by its global id (scenario_id0 + s, default
+        first + s).  Returns the device int32 [count, 2] initial positions if
+        init_pos, else None."""
+        prims = np.ascontiguousarray(generator_primitives(self.cookbook), dtype=np.int32)
+        ws = np.asarray([self.cookbook.index["workshop%d" % i] for i in range(self.params["N_WORKSHOPS"])],
+                        dtype=np.int32)
+        out = torch.empty((count, 2), dtype=torch.int32, device=self.device) if init_pos else None
+        sid0 = first if scenario_id0 is None else scenario_id0
+        self._check(N.lib().craft_pool_generate(
+            self._h, ctypes.c_uint64(seed & (2**64 - 1)), int(sid0), int(first), int(count),
+            self.cookbook.index["boundary"], prims.ctypes.data_as(ctypes.c_void_p), len(prims),
+            self.params["N_PRIMITIVES"], ws.ctypes.data_as(ctypes.c_void_p), len(ws), _ptr(out),
+            self._stream()), "craft_pool_generate")
+        self.pool_count = max(self.pool_count, first + count)
+        return out
+
     # ---- episodes -----------------------------------------------------------------------
     def reset(self, scenario, pos_x, pos_y, dir, task, obs=None):
         n = self.n_envs

@@ -207,3 +207,64 @@ def test_oracle_do_rollout_matches_reference(golden, oracle_mod, case, mode):
     assert [info["num_interactions"], info["num_steps"]] == fx[key + "_counts"].tolist()
     R = fx[key + "_received"]
     assert np.array_equal(np.asarray(info["received"], dtype=np.int8).reshape(R.shape), R)
+
+
+@pytest.mark.parametrize("name,world,count", [("w8", "craft_medium", 100), ("w12", "craft_medium_12x12", 64)])
+def test_oracle_generator_reproduces_reference_scenarios(golden, oracle_mod, name, world, count):
+    """oracle_generate_scenarios with numpy's RandomState stream == the reference's
+    make_data.sample_scenario (with its duplicate check): every grid, every initial
+    position, and the MT19937 state after the last draw."""
+    from psketch_amd.cookbook import generator_primitives
+    fx = golden("scenarios_seed123.npz")
+    params, cb, _, _ = make_tables(world)
+    ws = [cb.index["workshop%d" % i] for i in range(params["N_WORKSHOPS"])]
+    grids, init, mt = oracle_mod.generate_scenarios(
+        params["WIDTH"], params["HEIGHT"], cb.index["boundary"], generator_primitives(cb),
+        params["N_PRIMITIVES"], ws, count, 123, rng="mt19937", dedup=True)
+    assert np.array_equal(grids, fx[f"{name}_grids"])
+    assert np.array_equal(init, fx[f"{name}_init"])
+    assert np.array_equal(mt[:624], fx[f"{name}_mt_key"]) and mt[624] == fx[f"{name}_mt_pos"][0]
+
+
+def check_scenario_invariants(grids, init, W, H, boundary, prims, n_per, ws):
+    """What every make_data world satisfies: the boundary ring, the object counts,
+    one connected free region, every interior object next to a free cell, and a
+    free interior initial position that keeps both properties when occupied."""
+    from scipy import ndimage
+    g = grids.reshape(-1, W, H)
+    ring = np.zeros((W, H), bool)
+    ring[0, :] = ring[-1, :] = ring[:, 0] = ring[:, -1] = True
+    assert (g[:, ring] == boundary).all()
+    for k in prims:
+        assert ((g == k).sum(axis=(1, 2)) == n_per).all()
+    for k in ws:
+        assert ((g == k).sum(axis=(1, 2)) == 1).all()
+    n_obj = len(prims) * n_per + len(ws)
+    assert ((g[:, ~ring] != 0).sum(axis=1) == n_obj).all()
+    cross = ndimage.generate_binary_structure(2, 1)
+    for i in range(len(g)):
+        x, y = init[i]
+        assert 0 < x < W - 1 and 0 < y < H - 1 and g[i, x, y] == 0
+        occ = g[i] != 0
+        occ2 = occ.copy()
+        occ2[x, y] = True
+        for o in (occ, occ2):
+            _, ncomp = ndimage.label(~o, structure=cross)
+            assert ncomp == 1, i
+            free_nb = ndimage.binary_dilation(~o, structure=cross)
+            assert free_nb[o & ~ring].all(), i
+
+
+def test_oracle_splitmix_generator_invariants(oracle_mod):
+    from psketch_amd.cookbook import generator_primitives
+    params, cb, _, _ = make_tables("craft_large")
+    W, H = params["WIDTH"], params["HEIGHT"]
+    prims = generator_primitives(cb)
+    ws = [cb.index["workshop%d" % i] for i in range(params["N_WORKSHOPS"])]
+    grids, init, _ = oracle_mod.generate_scenarios(W, H, cb.index["boundary"], prims,
+                                                   params["N_PRIMITIVES"], ws, 300, 9)
+    check_scenario_invariants(grids, init, W, H, cb.index["boundary"], prims, params["N_PRIMITIVES"], ws)
+    # keyed by global id: any split of the ids gives the same worlds
+    g2, i2, _ = oracle_mod.generate_scenarios(W, H, cb.index["boundary"], prims, params["N_PRIMITIVES"],
+                                              ws, 100, 9, scenario_id0=200)
+    assert np.array_equal(g2, grids[200:]) and np.array_equal(i2, init[200:])
