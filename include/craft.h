@@ -239,6 +239,7 @@ typedef struct {
   int8_t* success;
   int32_t* action_record;          /* int32[n_envs] */
   int32_t* any_live;               /* int32 scalar flag */
+  int8_t* transition_code;         /* int8[n_envs]: see craft_transition; -1 if no step */
 } craft_step_args_t;
 int craft_step_ex(craft_sim_t* sim, const craft_step_args_t* args, void* stream);
 
@@ -265,9 +266,13 @@ int craft_stats(craft_sim_t* sim, int64_t* stats_out, int32_t reset, void* strea
 /* CraftState.step (craft.py:332-424) as a pure transition: slot dst[i] becomes
  * step(slot src[i], actions[i]) — src == dst updates in place, src != dst keeps
  * the old state (the reference's states are immutable).  actions[i] < 0 is a
- * no-op copy.  src/dst NULL = identity over n slots.  Device int32 arrays. */
+ * no-op copy.  src/dst NULL = identity over n slots.  Device int32 arrays.
+ * code_out (int8[n], may be NULL) receives what PrimitiveLanguageTeacher.describe
+ * reads off the (state, next state) pair (teachers/primitive_language.py:61-85):
+ * 0..3 = moved by the coord_change of DOWN/UP/LEFT/RIGHT, 4 = did not move and
+ * the inventory changed, 5 = neither, -1 = no step (action < 0). */
 int craft_transition(craft_sim_t* sim, const int32_t* src, const int32_t* dst,
-                     const int32_t* actions, int64_t n, void* stream);
+                     const int32_t* actions, int64_t n, int8_t* code_out, void* stream);
 
 /* CraftState.features() (craft.py:296-330) and satisfies() (craft.py:285-294)
  * for n slots (NULL = identity).  obs: [n][n_features] (obs format) or NULL; sat: int8[n]

@@ -10,7 +10,9 @@ from .cookbook import Cookbook, Index, Task, TaskManager, compile_config, world_
 from .sim import CraftSim, hash_actions, sample_scenarios, splitmix64, synthetic_specs
 from .dataset import Dataset
 from .rollout import ImitationRollout, RolloutInfo, do_rollout
+from .language import PrimitiveLanguageTeacher
 
 __all__ = ["gamedef", "Cookbook", "Index", "Task", "TaskManager", "compile_config",
            "world_params", "CraftSim", "hash_actions", "sample_scenarios", "splitmix64",
-           "synthetic_specs", "Dataset", "ImitationRollout", "RolloutInfo", "do_rollout"]
+           "synthetic_specs", "Dataset", "ImitationRollout", "RolloutInfo", "do_rollout",
+           "PrimitiveLanguageTeacher"]

@@ -85,6 +85,7 @@ class craft_step_args_t(ctypes.Structure):
         ("success", ctypes.c_void_p),
         ("action_record", ctypes.c_void_p),
         ("any_live", ctypes.c_void_p),
+        ("transition_code", ctypes.c_void_p),
     ]
 
 
@@ -117,7 +118,7 @@ SIGNATURES = {
     "craft_step_ex": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp]),
     "craft_rollout": (_i32, [_vp, _vp, _u64, _i64, _i32, _u32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "craft_stats": (_i32, [_vp, _vp, _i32, _vp]),
-    "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "craft_observe": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "craft_teacher": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "craft_get_state": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),

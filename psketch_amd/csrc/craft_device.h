@@ -114,6 +114,7 @@ struct TileArgs {
   const uint8_t* bc;
   int32_t* rec;
   int32_t* any_live;
+  int8_t* code;            // transition codes (craft_step_ex, craft_transition)
 };
 
 struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
@@ -199,6 +200,15 @@ __device__ __forceinline__ void mask_set(uint32_t (&m)[8], int c) {
 
 // CraftState.step (craft.py:332-424) on an LDS grid row `g` and inventory
 // bytes `iv`; `rc_tab` is the compact recipe table (LDS).  Records whether inventory / mask changed.
+// What PrimitiveLanguageTeacher.describe reads off a (state, next state) pair
+// (teachers/primitive_language.py:61-85): 0..3 = moved by the coord_change of
+// DOWN / UP / LEFT / RIGHT, 4 = did not move and the inventory changed, 5 = neither.
+__device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, bool inv_changed) {
+  const int dx = s.x - ox, dy = s.y - oy;
+  if (dx == 0 && dy == 0) return inv_changed ? 4 : 5;
+  return dy < 0 ? CRAFT_DOWN : dy > 0 ? CRAFT_UP : dx < 0 ? CRAFT_LEFT : CRAFT_RIGHT;
+}
+
 __device__ __forceinline__ void transition(const SimView& v, const uint8_t* rc_tab, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
                                            bool& mask_changed) {

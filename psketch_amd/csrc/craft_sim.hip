@@ -537,6 +537,7 @@ int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
   a.bc = x->behavior_clone;
   a.rec = x->action_record;
   a.any_live = x->any_live;
+  a.code = x->transition_code;
   return launch(s, craft::MODE_TICK, a, stream, "craft_step launch");
 }
 
@@ -581,7 +582,7 @@ int craft_stats(craft_sim_t* s, int64_t* stats_out, int32_t reset, void* stream)
 }
 
 int craft_transition(craft_sim_t* s, const int32_t* src, const int32_t* dst, const int32_t* actions,
-                     int64_t n, void* stream) {
+                     int64_t n, int8_t* code_out, void* stream) {
   if (!s || !actions || n < 0) return fail(s, CRAFT_EINVAL, "craft_transition: bad argument");
   if (!src && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_transition: n > n_envs");
   TileArgs a{};
@@ -589,6 +590,7 @@ int craft_transition(craft_sim_t* s, const int32_t* src, const int32_t* dst, con
   a.dst = dst;
   a.actions = actions;
   a.n = n;
+  a.code = code_out;
   return launch(s, craft::MODE_TRANSITION, a, stream, "craft_transition launch");
 }
 

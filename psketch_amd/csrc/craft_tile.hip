@@ -127,6 +127,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
     ivw[4] = i1.x; ivw[5] = i1.y; ivw[6] = i1.z; ivw[7] = i1.w;
     bool inv_changed = false, mask_changed = false;
     int d = 0, succ = -1, counted = 0;
+    int code = -1;                                         // transition code (craft.h)
     if (live) {
       // The LDS row holds pool[scenario]; cells cleared this episode are applied
       // lazily, so an auto-reset (which restores exactly that row) needs no reload.
@@ -177,12 +178,22 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
           s.frozen = 1;
           s.timer = max(s.timer, 0);
         } else if (!d) {
-          if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-          else transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+          if (act < 0 || act >= CRAFT_N_ACTIONS) {
+            latch_error(v.err, CRAFT_EBADACTION, slot);
+          } else {
+            const int ox = s.x, oy = s.y;
+            transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+            code = transition_code(ox, oy, s, inv_changed);
+          }
         }
       } else if (MODE == MODE_TRANSITION) {
-        if (act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-        else if (act >= 0) transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+        if (act >= CRAFT_N_ACTIONS) {
+          latch_error(v.err, CRAFT_EBADACTION, slot);
+        } else if (act >= 0) {
+          const int ox = s.x, oy = s.y;
+          transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+          code = transition_code(ox, oy, s, inv_changed);
+        }
         if (dslot != slot) inv_changed = mask_changed = true;   // copy-on-step
       } else if (MODE == MODE_OBSERVE) {
         if (a.sat) {
@@ -215,6 +226,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
         if (a.rec) a.rec[i] = counted ? act : -1;        // action_seqs, imitation.py:59-61
       }
     }
+    if ((MODE == MODE_TICK || MODE == MODE_TRANSITION) && a.code && tid < nE) a.code[env0 + tid] = (int8_t)code;
     s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
     if (MODE == MODE_TICK) {
       // episode statistics: one partial-sum row per workgroup (uncontended)

@@ -175,7 +175,7 @@ class CraftSim:
 
     def step(self, actions=None, seed=0, tick=0, autoreset=True, obs=None, reward=None, done=None,
              success=None, ref_actions=None, behavior_clone=None, action_record=None,
-             any_live=None):
+             any_live=None, transition_code=None):
         """One rollout tick for every slot (include/craft.h craft_step / craft_step_ex).
         actions: int32 device tensor [N] or None for the in-kernel hashed draw;
         ref_actions + behavior_clone (uint8 [N]): cloned actions; action_record
@@ -184,7 +184,7 @@ class CraftSim:
         n = self.n_envs
         flags = N.STEP_AUTORESET if autoreset else 0
         if ref_actions is None and behavior_clone is None and action_record is None \
-                and any_live is None:
+                and any_live is None and transition_code is None:
             # plain tick: the short craft_step entry (least host overhead per launch)
             a = self._i32(actions, n) if actions is not None else None
             self._check(N.lib().craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
@@ -209,7 +209,8 @@ class CraftSim:
             put("behavior_clone", bc)
         for name, t, dt in (("reward", reward, torch.float32), ("done", done, torch.uint8),
                             ("success", success, torch.int8), ("action_record", action_record, torch.int32),
-                            ("any_live", any_live, torch.int32)):
+                            ("any_live", any_live, torch.int32),
+                            ("transition_code", transition_code, torch.int8)):
             if t is not None and (t.dtype != dt or not t.is_contiguous()):
                 raise TypeError(f"{name} must be a contiguous {dt} tensor")
             put(name, t)
@@ -259,12 +260,17 @@ class CraftSim:
         return out
 
     # ---- reference-granular surface ----------------------------------------------------
-    def transition(self, actions, src=None, dst=None):
+    def transition(self, actions, src=None, dst=None, codes=None):
+        """CraftState.step per item (craft_transition); codes: int8 [n] device
+        tensor receiving the describe() transition code of each item."""
         a = self._i32(actions)
         n = a.numel()
         s, d = self._i32(src, n), self._i32(dst, n)
-        self._check(N.lib().craft_transition(self._h, _ptr(s), _ptr(d), _ptr(a), n, self._stream()),
-                    "craft_transition")
+        if codes is not None and (codes.dtype != torch.int8 or codes.numel() != n):
+            raise TypeError(f"codes must be an int8 tensor of {n} entries")
+        self._check(N.lib().craft_transition(self._h, _ptr(s), _ptr(d), _ptr(a), n, _ptr(codes),
+                                             self._stream()), "craft_transition")
+        return codes
 
     def observe(self, slots=None, tasks=None, obs=None, sat=None, n=None):
         s = self._i32(slots)

@@ -582,7 +582,61 @@ def gen_imitation(w12_grids):
     print("imitation_rollout.npz", os.path.getsize(os.path.join(OUT, "imitation_rollout.npz")))
 
 
+def gen_language(w12_grids):
+    """PrimitiveLanguageTeacher.describe / instruct (teachers/primitive_language.py:17-90)
+    run by the reference on random 12x12 rollouts: (1) one-action calls env by env
+    each tick, sharing one teacher, as trainers/interactive_primitive_language.py:55-68
+    calls it; (2) whole-sequence calls with a fresh teacher per env."""
+    cfg, world = make_world(12, 3)
+    cfg.teacher = util.Struct(name="PrimitiveLanguageTeacher")
+    K = world.cookbook.n_kinds
+    rng = np.random.RandomState(31)
+    B, T = 64, 30
+    pool = w12_grids[:16]
+    spec, states = [], []
+    for e in range(B):
+        sc = e % len(pool)
+        g = pool[sc].reshape(12, 12)
+        free = [(x, y) for x in range(1, 11) for y in range(1, 11) if g[x, y] == 0]
+        x, y = free[rng.randint(len(free))]
+        d = rng.randint(4)
+        spec.append([sc, x, y, d])
+        states.append(world.init_state(ids_to_onehot(g, K), (x, y), d))
+    actions = rng.randint(0, 6, size=(T, B))
+    cfg.random = np.random.RandomState(5)
+    teacher = teachers.load(cfg)
+    desc1, seqs = [], [[s] for s in states]
+    for t in range(T):
+        row = []
+        for i in range(B):
+            prev = states[i]
+            _, states[i] = prev.step(int(actions[t, i]))
+            seqs[i].append(states[i])
+            row.append(teacher.describe(world, [int(actions[t, i])], [prev, states[i]])[0])
+        desc1.append(row)
+    map1 = sorted((int(k), v) for k, v in teacher.student_action_map.items())
+    desc2 = []
+    for i in range(B):
+        t2 = teachers.load(cfg)
+        t2.random = np.random.RandomState(100 + i)
+        desc2.append(t2.describe(world, [int(a) for a in actions[:, i]], seqs[i]))
+    instr = [teacher.instruct(world, [int(a) for a in actions[:, i]]) for i in range(4)]
+    words = ["down", "up", "left", "right", "use", "stop"]
+    enc = lambda ws: np.asarray([words.index(w) for w in ws], dtype=np.int8)  # noqa: E731
+    np.savez_compressed(os.path.join(OUT, "language.npz"),
+                        pool=np.asarray(pool, dtype=np.uint8), spec=np.asarray(spec, dtype=np.int32),
+                        actions=actions.astype(np.int8),
+                        desc_tick=np.stack([enc(r) for r in desc1]),
+                        map_tick=np.asarray([[k, words.index(v)] for k, v in map1], dtype=np.int8),
+                        desc_seq=np.stack([enc(r) for r in desc2]),
+                        instruct=np.stack([enc(r) for r in instr]))
+    print("language.npz", len(map1), "map entries;", os.path.getsize(os.path.join(OUT, "language.npz")))
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["language"]:            # only the language-teacher fixture
+        gen_language(np.load(os.path.join(OUT, "scenarios_seed123.npz"))["w12_grids"])
+        sys.exit(0)
     if sys.argv[1:] == ["imitation"]:           # only the do_rollout fixture
         gen_imitation(np.load(os.path.join(OUT, "scenarios_seed123.npz"))["w12_grids"])
         sys.exit(0)
@@ -595,3 +649,4 @@ if __name__ == "__main__":
     gen_rollout(sc["w12_grids"], 3, T=100, E=64, P=16, all_obs_ticks=None)
     gen_rollout(sc["w12_grids"], 5, T=60, E=48, P=16, all_obs_ticks=None)
     gen_imitation(sc["w12_grids"])
+    gen_language(sc["w12_grids"])

@@ -268,3 +268,44 @@ def test_oracle_splitmix_generator_invariants(oracle_mod):
     g2, i2, _ = oracle_mod.generate_scenarios(W, H, cb.index["boundary"], prims, params["N_PRIMITIVES"],
                                               ws, 100, 9, scenario_id0=200)
     assert np.array_equal(g2, grids[200:]) and np.array_equal(i2, init[200:])
+
+
+def _language_codes_from_oracle(oracle_mod, fx):
+    """Transition codes of the fixture's rollout, from the oracle's states."""
+    from psketch_amd.language import codes_from_states
+    _, _, _, cfg = make_tables("craft_medium_12x12")
+    orc = oracle_mod.Oracle(cfg)
+    pool, spec, actions = fx["pool"], fx["spec"], fx["actions"]
+    envs = [orc.env(pool[sc], x, y, d) for sc, x, y, d in spec]
+    T, B = actions.shape
+    codes = np.zeros((T, B), dtype=np.int8)
+    for t in range(T):
+        for i in range(B):
+            e = envs[i]
+            p0, inv0 = (int(e["x"][0]), int(e["y"][0])), e["inv"][0].copy()
+            assert orc.step(e, int(actions[t, i])) == 0
+            codes[t, i] = codes_from_states(p0, (int(e["x"][0]), int(e["y"][0])), inv0, e["inv"][0])
+    return codes
+
+
+def test_language_teacher_matches_reference(golden, oracle_mod):
+    """psketch_amd.language.PrimitiveLanguageTeacher == the reference's
+    describe / instruct (teachers/primitive_language.py:17-90): one-action calls
+    env by env with one shared teacher, whole-sequence calls with fresh teachers,
+    the learned action map, and the same RandomState draws."""
+    from psketch_amd.language import WORDS, PrimitiveLanguageTeacher
+    fx = golden("language.npz")
+    codes = _language_codes_from_oracle(oracle_mod, fx)
+    actions = fx["actions"]
+    T, B = actions.shape
+    teacher = PrimitiveLanguageTeacher(np.random.RandomState(5))
+    got = [teacher.describe_batch(actions[t], codes[t]) for t in range(T)]
+    assert [[WORDS.index(w) for w in row] for row in got] == fx["desc_tick"].tolist()
+    assert sorted((k, WORDS.index(v)) for k, v in teacher.student_action_map.items()) == \
+        [tuple(r) for r in fx["map_tick"].tolist()]
+    for i in range(B):
+        t2 = PrimitiveLanguageTeacher(np.random.RandomState(100 + i))
+        d = t2.describe_codes(actions[:, i], codes[:, i])
+        assert [WORDS.index(w) for w in d] == fx["desc_seq"][i].tolist(), i
+    for i in range(len(fx["instruct"])):
+        assert [WORDS.index(w) for w in teacher.instruct(None, actions[:, i])] == fx["instruct"][i].tolist()
