@@ -96,5 +96,21 @@ __device__ __forceinline__ Bits<NW> bshift(const Bits<NW>& a, int d) {
   }
   return r;
 }
+// bshift for a shift amount known only at run time (the alignbit amount is a VGPR).
+template <int NW>
+__device__ __forceinline__ Bits<NW> bshift_var(const Bits<NW>& a, int d) {
+  Bits<NW> r;
+  if (d > 0) {
+    r.w[0] = a.w[0] << d;
+#pragma unroll
+    for (int i = 1; i < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i], a.w[i - 1], 32 - d);
+  } else {
+    const int s = -d;
+#pragma unroll
+    for (int i = 0; i + 1 < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i + 1], a.w[i], s);
+    r.w[NW - 1] = a.w[NW - 1] >> s;
+  }
+  return r;
+}
 
 }  // namespace craft

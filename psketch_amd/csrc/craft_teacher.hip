@@ -1,104 +1,203 @@
 // craft_teacher.hip — DemonstrationTeacher on the GPU: the hint-tree walk of
-// BaseTeacher.find_incomplete_subtask and find_closest_resources' BFS, one lane
-// per env, the BFS held as per-direction position bitsets in registers.
+// BaseTeacher.find_incomplete_subtask and find_closest_resources' BFS, one quad
+// of lanes per env, the BFS held as per-direction position bitsets in registers.
 #include "craft_bits.h"
 
 namespace craft {
 
 // find_closest_resources (teachers/base.py:27-34) over shortest_path
-// (teachers/base.py:36-87) as ONE level-synchronous BFS over (pos, dir) states
-// held as per-direction position bitsets.  FIFO order within a level is
-// sorted by the path's first action (induction: level 1 is enqueued in action
-// order DOWN, UP, LEFT, RIGHT, and children keep their first-dequeued parent's
-// label), so tracking the level's states per first action (a "label")
-// reproduces exactly which state the reference dequeues first:
-//   a target's path length = the first level at which a state faces it,
-//   its first action = the smallest label among that level's facing states,
-//   the chosen target = the first in np.nonzero (x-major) order with the
-//   minimal length (strict `<`, base.py:31).
-// Returns false where the reference raises (len(None) on an unreachable
-// target after a reachable one, base.py:31).
+// (teachers/base.py:36-87), exactly, with one forward and one backward BFS over
+// (pos, dir) states held as per-direction position bitsets.
+//
+// What the reference returns.  Each target's own FIFO BFS dequeues level by level,
+// and within a level in order of the path's first action (level 1 is enqueued in
+// action order DOWN, UP, LEFT, RIGHT; a child keeps its first-dequeued parent's
+// label).  So a target's path length L is the first level at which a state faces
+// it, and its first action is the smallest first action over all shortest paths
+// to a state facing it.  The chosen target is the first in np.nonzero (x-major)
+// order with the minimal L (strict `<`, base.py:31).
+//
+// How it is computed here.
+//  * Forward: a move's result does not depend on the current direction, so level
+//    k+1 in direction a is (shift(U_k, d_a) & free | U_k & blocked_a) minus the
+//    visited set of direction a, U_k being the positions of level k.  A level's
+//    facing cells are its states shifted once more.  This gives every target's L
+//    and the chosen target, in ~40 bitset operations per level.
+//  * Backward, for the chosen target only: reverse BFS from the states facing it
+//    for L-1 levels; the first action is the smallest a whose level-1 state
+//    step(start, a) is within reverse distance L-1 (then exactly L-1).
+// Returns false where the reference raises (len(None) on an unreachable target
+// after a reachable one, base.py:31): the forward BFS then runs until its
+// frontier is empty, so `claimed` holds every reachable target.
+// One lane per query (LANES = 1): the same forward and backward passes, the four
+// actions of a level in one lane.
 template <int NW>
-__device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
-                            int H, int p0, int d0, int& first_action, int& path_len) {
+__device__ bool bfs_closest_1(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
+                              int H, int p0, int d0, int& first_action, int& path_len,
+                              bool want_action) {
   const int dl[4] = {-1, 1, -H, H};   // DOWN, UP, LEFT, RIGHT in x-major cell index
   const Bits<NW> fr = bandn(valid, occ);
-  Bits<NW> V[4], cur[4], fc[4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) V[a] = bzero<NW>();
-#pragma unroll
-  for (int a = 0; a < 4; ++a) V[a] = (a == d0) ? bbit<NW>(p0) : V[a];
-  Bits<NW> claimed = bzero<NW>();
-  bool found = false;
-  first_action = -1;
-  path_len = -1;
-  {
-    const int f0 = p0 + dl[d0];            // start state already faces a target: []
-    if (f0 >= 0 && btest(tgt, f0)) {
-      found = true;
-      path_len = 0;
-      claimed = bbit<NW>(f0);
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int q0 = p0 + dl[a];
-    const int q = btest(fr, q0) ? q0 : p0;
-    if (!btest(V[a], q)) {
-      V[a] = bor(V[a], bbit<NW>(q));
-      cur[a] = bbit<NW>(q);
-      fc[a] = band(bshift(cur[a], dl[a]), valid);
-    } else {
-      cur[a] = bzero<NW>();
-      fc[a] = bzero<NW>();
-    }
-  }
   Bits<NW> blk[4];
 #pragma unroll
   for (int a = 0; a < 4; ++a) blk[a] = bshift(occ, -dl[a]);   // blk[a][p] = occ[p + dl[a]]
-  int depth = 1;
-  while (bany(bor(bor(cur[0], cur[1]), bor(cur[2], cur[3])))) {
-    int bp = INT_MAX, bl = -1;
-#pragma unroll
-    for (int lab = 0; lab < 4; ++lab) {
-      const Bits<NW> hit = bandn(band(fc[lab], tgt), claimed);
-      if (bany(hit)) {
-        claimed = bor(claimed, hit);
-        const int p = blowest(hit);
-        if (p < bp) { bp = p; bl = lab; }
-      }
+  first_action = -1;
+  path_len = -1;
+  Bits<NW> claimed = bzero<NW>();
+  int L = -1, chosen = -1;
+  {
+    const int f0 = p0 + dl[d0];            // the start state already faces a target: []
+    if (f0 >= 0 && btest(tgt, f0)) {
+      L = 0;
+      chosen = f0;
+      claimed = bbit<NW>(f0);
     }
-    if (!found && bl >= 0) {
-      found = true;
-      path_len = depth;
-      first_action = bl;
-    }
-    if (!bany(bandn(tgt, claimed))) break;
-    // Expand label by label, in place: a label's current set is only needed for
-    // its own expansion, and V[a] (updated immediately) gives smaller labels priority.
-#pragma unroll
-    for (int lab = 0; lab < 4; ++lab) {
-      Bits<NW> nc = bzero<NW>(), nf = bzero<NW>();
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const Bits<NW> moved = bor(band(bshift(cur[lab], dl[a]), fr), band(cur[lab], blk[a]));
-        const Bits<NW> fresh = bandn(moved, V[a]);
-        V[a] = bor(V[a], fresh);
-        nc = bor(nc, fresh);
-        nf = bor(nf, band(bshift(fresh, dl[a]), valid));
-      }
-      cur[lab] = nc;
-      fc[lab] = nf;
-    }
-    ++depth;
   }
-  if (found) {
-    const Bits<NW> unreached = bandn(tgt, claimed);
-    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  Bits<NW> V[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) V[a] = (a == d0) ? bbit<NW>(p0) : bzero<NW>();
+  Bits<NW> U = bbit<NW>(p0);
+  for (int depth = 1; bany(bandn(tgt, claimed)); ++depth) {
+    Bits<NW> nU = bzero<NW>(), hit = bzero<NW>();
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const Bits<NW> nxt = bandn(bor(band(bshift(U, dl[a]), fr), band(U, blk[a])), V[a]);
+      V[a] = bor(V[a], nxt);
+      nU = bor(nU, nxt);
+      hit = bor(hit, band(bshift(nxt, dl[a]), tgt));
+    }
+    if (!bany(nU)) break;                  // every reachable state visited
+    hit = bandn(hit, claimed);
+    if (bany(hit)) {
+      claimed = bor(claimed, hit);
+      if (L < 0) {
+        L = depth;
+        chosen = blowest(hit);
+      }
+    }
+    U = nU;
+  }
+  if (L < 0) return true;                  // no target at all, or none reachable: None
+  path_len = L;
+  const Bits<NW> unreached = bandn(tgt, claimed);
+  if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  if (L == 0 || !want_action) return true;
+  Bits<NW> G[4];                           // reverse BFS from the states facing `chosen`
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int q = chosen - dl[a];
+    G[a] = (q >= 0) ? band(bbit<NW>(q), fr) : bzero<NW>();
+    V[a] = G[a];
+  }
+  for (int k = 1; k < L; ++k) {
+    Bits<NW> P = bzero<NW>();              // predecessors: any direction at these positions
+#pragma unroll
+    for (int a = 0; a < 4; ++a) P = bor(P, bor(band(bshift(G[a], -dl[a]), fr), band(G[a], blk[a])));
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      G[a] = bandn(P, V[a]);
+      V[a] = bor(V[a], G[a]);
+    }
+  }
+#pragma unroll
+  for (int a = 3; a >= 0; --a) {           // the smallest qualifying action wins
+    const int q0 = p0 + dl[a];
+    const int q = btest(fr, q0) ? q0 : p0;
+    if (!(q == p0 && a == d0) && btest(V[a], q)) first_action = a;
   }
   return true;
 }
 
+// OR over the 4 lanes of a quad (DPP quad_perm [1,0,3,2] then [2,3,0,1]).
+__device__ __forceinline__ uint32_t quad_or(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+  x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+  return x;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> quad_or(const Bits<NW>& a) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = quad_or(a.w[i]);
+  return r;
+}
+
+// LANES = 4: the four lanes of a quad run one query together, lane ql handling the states
+// entered by action ql (its direction's visited set and blocked mask): each
+// level is then one action's worth of bitset work plus two quad ORs, instead of
+// four actions' worth in one lane.  Every quantity that steers control flow is
+// quad-uniform.
+template <int NW, int LANES>
+__device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
+                            int H, int p0, int d0, int ql, int& first_action, int& path_len,
+                            bool want_action = true) {
+  if (LANES == 1) return bfs_closest_1<NW>(occ, tgt, valid, H, p0, d0, first_action, path_len, want_action);
+  const int dla = ql == 0 ? -1 : ql == 1 ? 1 : ql == 2 ? -H : H;   // this lane's action
+  const Bits<NW> fr = bandn(valid, occ);
+  const Bits<NW> blk = bshift_var(occ, -dla);                         // blk[p] = occ[p + dla]
+  const int dl0 = d0 == 0 ? -1 : d0 == 1 ? 1 : d0 == 2 ? -H : H;
+  first_action = -1;
+  path_len = -1;
+  Bits<NW> claimed = bzero<NW>();
+  int L = -1, chosen = -1;
+  {
+    const int f0 = p0 + dl0;               // the start state already faces a target: []
+    if (f0 >= 0 && btest(tgt, f0)) {
+      L = 0;
+      chosen = f0;
+      claimed = bbit<NW>(f0);
+    }
+  }
+  Bits<NW> V = (ql == d0) ? bbit<NW>(p0) : bzero<NW>();   // visited states of direction ql
+  Bits<NW> U = bbit<NW>(p0);
+  for (int depth = 1; bany(bandn(tgt, claimed)); ++depth) {
+    const Bits<NW> nxt = bandn(bor(band(bshift_var(U, dla), fr), band(U, blk)), V);
+    V = bor(V, nxt);
+    const Bits<NW> nU = quad_or(nxt);
+    Bits<NW> hit = quad_or(band(bshift_var(nxt, dla), tgt));
+    if (!bany(nU)) break;                  // every reachable state visited
+    hit = bandn(hit, claimed);
+    if (bany(hit)) {
+      claimed = bor(claimed, hit);
+      if (L < 0) {
+        L = depth;
+        chosen = blowest(hit);
+      }
+    }
+    U = nU;
+  }
+  if (L < 0) return true;                  // no target at all, or none reachable: None
+  path_len = L;
+  const Bits<NW> unreached = bandn(tgt, claimed);
+  if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  if (L == 0 || !want_action) return true;
+  // reverse BFS from the states facing `chosen`; G = this level's states of direction
+  // ql, V reused as the reverse-visited set
+  Bits<NW> G;
+  {
+    const int q = chosen - dla;
+    G = (q >= 0) ? band(bbit<NW>(q), fr) : bzero<NW>();
+    V = G;
+  }
+  for (int k = 1; k < L; ++k) {
+    // predecessors, any direction, at these positions: moved here or turned in place
+    const Bits<NW> P = quad_or(bor(band(bshift_var(G, -dla), fr), band(G, blk)));
+    G = bandn(P, V);
+    V = bor(V, G);
+  }
+  // the smallest action whose level-1 state lies within reverse distance L-1
+  const int q0 = p0 + dla;
+  const int q = btest(fr, q0) ? q0 : p0;
+  const bool ok = !(q == p0 && ql == d0) && btest(V, q);
+  const uint64_t b = __ballot(ok);
+  const uint32_t quad = (uint32_t)(b >> (__lane_id() & ~3u)) & 0xfu;
+  first_action = quad ? __ffs(quad) - 1 : -1;
+  return true;
+}
+
+
+// Batches up to this many items run 4 lanes per item (tools/teacher_bench.py:
+// latency-bound below it, throughput-bound above).
+constexpr int64_t kTeacherQuadMaxItems = 32768;
 
 struct TeachArgs {
   const int32_t* slots;
@@ -117,34 +216,47 @@ __device__ __forceinline__ int grid_kind(const SimView& v, int scen, const uint3
 }
 
 // DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30), one lane per slot.
-template <int NW>
+// LANES lanes per item: 4 (quad-parallel BFS) shortens each query's dependent
+// chain, which is what bounds a small batch; 1 does the least total work, which is
+// what bounds a large one (launch_teacher picks by batch size).
+template <int NW, int LANES>
 __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
+  const int ql = LANES == 4 ? (threadIdx.x & 3) : 0;
+  if (i >= a.n) return;                  // lane-group-uniform: a group never straddles two items
+  const bool lead = ql == 0;             // the lane that writes the outputs and latches errors
   const int64_t slot = a.slots ? (int64_t)a.slots[i] : i;
   if (slot == -1) {                    // skipped item: the trainer's ref_action for a done env
-    a.act_out[i] = -1;
-    if (a.len_out) a.len_out[i] = -1;
+    if (lead) {
+      a.act_out[i] = -1;
+      if (a.len_out) a.len_out[i] = -1;
+    }
     return;
   }
   if (slot < 0 || slot >= v.n_envs) {
-    latch_error(v.err, CRAFT_ERANGE, i);
-    a.act_out[i] = -2;
-    if (a.len_out) a.len_out[i] = -2;
+    if (lead) {
+      latch_error(v.err, CRAFT_ERANGE, i);
+      a.act_out[i] = -2;
+      if (a.len_out) a.len_out[i] = -2;
+    }
     return;
   }
   const Agent s = unpack_state(v.state[slot]);
   if (s.frozen) {                      // done env: its label is -1 (imitation.py:50-51)
-    a.act_out[i] = -1;
-    if (a.len_out) a.len_out[i] = -1;
+    if (lead) {
+      a.act_out[i] = -1;
+      if (a.len_out) a.len_out[i] = -1;
+    }
     return;
   }
   const int task = a.tasks ? a.tasks[i] : s.task;
   if (task < 0 || task >= v.n_tasks || s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 ||
       s.scen >= v.pool_count) {
-    latch_error(v.err, task < 0 || task >= v.n_tasks ? CRAFT_ERANGE : CRAFT_EINVAL, i);
-    a.act_out[i] = -2;
-    if (a.len_out) a.len_out[i] = -2;
+    if (lead) {
+      latch_error(v.err, task < 0 || task >= v.n_tasks ? CRAFT_ERANGE : CRAFT_EINVAL, i);
+      a.act_out[i] = -2;
+      if (a.len_out) a.len_out[i] = -2;
+    }
     return;
   }
   uint32_t m[8];
@@ -195,10 +307,10 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
       }
     }
   };
-  auto closest = [&](int kind, int& fa, int& len) -> bool {
+  auto closest = [&](int kind, int& fa, int& len, bool want_action) -> bool {
     Bits<NW> occ, tgt;
     grids(kind, occ, tgt);
-    return bfs_closest<NW>(occ, tgt, valid, H, s.x * H + s.y, s.dir, fa, len);
+    return bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y, s.dir, ql, fa, len, want_action);
   };
   int leaf_kind = -1, leaf_fa = -1, leaf_len = -1;
   bool leaf_ok = true;
@@ -226,7 +338,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
         action = CRAFT_USE;
       } else if (goal == CRAFT_GOAL_GO) {
         int fa = -1, len = -1;
-        leaf_ok = closest(arg, fa, len);
+        leaf_ok = closest(arg, fa, len, true);
         leaf_kind = arg; leaf_fa = fa; leaf_len = len;
         if (!leaf_ok) err = CRAFT_ETEACHER;
         else if (len < 0) action = CRAFT_STOP;                           // demonstration.py:25-26
@@ -238,35 +350,42 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
     }
   }
   if (err) {
-    latch_error(v.err, err, slot);
+    if (lead) latch_error(v.err, err, slot);
     action = -2;                       // where the reference raises
   }
-  a.act_out[i] = action;
+  if (lead) a.act_out[i] = action;
   if (a.len_out) {
     const int arg = (v.task_tab[task] >> 4) & 0xff;
     int fa = leaf_fa, len = leaf_len;
     bool ok = leaf_ok;
     if (arg != leaf_kind) {               // the teacher's BFS already answered get[X]'s go[X]
       len = -1;
-      ok = arg > 0 ? closest(arg, fa, len) : true;
+      ok = arg > 0 ? closest(arg, fa, len, false) : true;
     }
     if (!ok) {
-      latch_error(v.err, CRAFT_ETEACHER, slot);
+      if (lead) latch_error(v.err, CRAFT_ETEACHER, slot);
       len = -2;
     }
-    a.len_out[i] = len;
+    if (lead) a.len_out[i] = len;
   }
 }
 
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
   TeachArgs a{slots, tasks, n, act_out, len_out};
-  const unsigned blocks = (unsigned)((n + 255) / 256);
   // nw = 32-bit words per cell set: 8x8 -> 2, 10x10 -> 4, 12x12 -> 5, 16x16 -> 8
-  if (nw <= 2) hipLaunchKernelGGL(teacher_kernel<2>, dim3(blocks), dim3(256), 0, st, v, a);
-  else if (nw <= 4) hipLaunchKernelGGL(teacher_kernel<4>, dim3(blocks), dim3(256), 0, st, v, a);
-  else if (nw <= 5) hipLaunchKernelGGL(teacher_kernel<5>, dim3(blocks), dim3(256), 0, st, v, a);
-  else hipLaunchKernelGGL(teacher_kernel<8>, dim3(blocks), dim3(256), 0, st, v, a);
+  const bool quad = n <= kTeacherQuadMaxItems;
+  const unsigned blocks = (unsigned)(((quad ? 4 : 1) * n + 255) / 256);
+#define CRAFT_TEACH(NWV)                                                                           \
+  do {                                                                                             \
+    if (quad) hipLaunchKernelGGL((teacher_kernel<NWV, 4>), dim3(blocks), dim3(256), 0, st, v, a);  \
+    else hipLaunchKernelGGL((teacher_kernel<NWV, 1>), dim3(blocks), dim3(256), 0, st, v, a);       \
+  } while (0)
+  if (nw <= 2) CRAFT_TEACH(2);
+  else if (nw <= 4) CRAFT_TEACH(4);
+  else if (nw <= 5) CRAFT_TEACH(5);
+  else CRAFT_TEACH(8);
+#undef CRAFT_TEACH
   return hipGetLastError();
 }
 

@@ -15,8 +15,8 @@ def timeit(fn, iters=100, warm=10):
     return a.elapsed_time(b) / iters * 1e3
 
 out = {}
-for world in sys.argv[1:] or ["craft_medium_12x12"]:
-    n = 65536
+sizes = [int(x) for x in os.environ.get("TEACHER_ENVS", "65536").split(",")]
+for world, n in [(w, n) for w in (sys.argv[1:] or ["craft_medium_12x12"]) for n in sizes]:
     sim = CraftSim(world, n_envs=n, device=0, pool_capacity=1024)
     g, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, 1024)
     sim.load_pool(g)
@@ -37,5 +37,5 @@ for world in sys.argv[1:] or ["craft_medium_12x12"]:
          "tick_plus_teacher_us": timeit(both)}
     r["config5_env_steps_per_s"] = n / (r["tick_plus_teacher_us"] * 1e-6)
     sim.check()
-    out[world] = {k: round(v, 2) for k, v in r.items()}
+    out[f"{world}/{n}"] = {k: round(v, 2) for k, v in r.items()}
 print(json.dumps(out, indent=1))
