@@ -35,6 +35,7 @@
 namespace craft {
 
 typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 // NT threads per workgroup: wave 0 runs the transitions, waves 1.. stream.
 template <int WIN, int TILE, int NT>
@@ -259,10 +260,12 @@ __global__ __launch_bounds__(NT, WIN == 3 ? 4 : 2) void rollout_kernel(SimView v
     // ---- publish the tile for the unit (t, c + 1): its state, and every output this unit wrote ----
     // (a later unit may rewrite the same ring slots from another XCD, so the release must cover
     // the observation stores of all waves, not only the state)
+    // When no ring slot is written twice in this launch (ring >= n_ticks), only the state
+    // passes between units: it is stored write-through (sc1) and published with no
+    // release fence (Guideline 16 R1), which leaves this XCD's L2 alone.
+    const bool state_only = a.ring >= a.n_ticks;
+    const bool handoff = c + 1 < n_chunks;
     if (tid < TILE && live) {
-      v.state[slot] = st;
-      v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
-      v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
       // this episode's cleared cells: non-empty in pool[scenario], empty in the LDS row
       const uint32_t* row = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
       const uint32_t* cur = reinterpret_cast<const uint32_t*>(g);
@@ -276,10 +279,33 @@ __global__ __launch_bounds__(NT, WIN == 3 ? 4 : 2) void rollout_kernel(SimView v
           if (cleared) m[cell >> 5] |= 1u << (cell & 31);
         }
       }
-      v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
-      v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
+      if (handoff && state_only) {
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t inv_r = __builtin_amdgcn_make_buffer_rsrc(v.inv, 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t msk_r = __builtin_amdgcn_make_buffer_rsrc(v.mask, 0, 0x7fffffff, 0x00020000);
+        const int off = (int)(slot * 32);
+        __hip_atomic_store((gu64*)(v.state + slot), (unsigned long long)st, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[0], ivw[1], ivw[2], ivw[3]}, inv_r, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[4], ivw[5], ivw[6], ivw[7]}, inv_r, off + 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{m[0], m[1], m[2], m[3]}, msk_r, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{m[4], m[5], m[6], m[7]}, msk_r, off + 16, 0, 16);
+      } else {
+        v.state[slot] = st;
+        v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+        v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
+        v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
+        v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
+      }
     }
-    if (c + 1 < n_chunks) {
+    if (handoff && state_only) {
+      if (tid < 64) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the storing wave drains
+        if (tid == 0)
+          __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (handoff) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains
       __syncthreads();
       if (tid == 0) {

@@ -386,26 +386,28 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
     sim.check()
 
 
-@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given,chunk", [
-    ("craft_medium_12x12", 12, 0, "f32", True, False, 0),
-    ("craft_medium_12x12", 12, 0, "f32", True, False, 1),
-    ("craft_medium_12x12", 12, 16, "bf16", True, True, 2),
-    ("craft_medium_12x12", 12, 32, "u8", False, True, 3),
-    ("craft_medium_12x12_w5", 12, 0, "f32", True, False, 2),
-    ("craft_16x16_w7", 16, 0, "f32", False, False, 0),
-    ("craft_medium", 8, 64, "f32", True, True, 1)])
-def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, chunk):
+@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given,chunk,R", [
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 0, 3),
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 1, 3),
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 1, 16),
+    ("craft_medium_12x12", 12, 16, "bf16", True, True, 2, 3),
+    ("craft_medium_12x12", 12, 32, "u8", False, True, 3, 16),
+    ("craft_medium_12x12_w5", 12, 0, "f32", True, False, 2, 3),
+    ("craft_16x16_w7", 16, 0, "f32", False, False, 0, 3),
+    ("craft_medium", 8, 64, "f32", True, True, 1, 9)])
+def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, chunk, R):
     """craft_rollout(K ticks) == K craft_step calls: observation / reward / done /
     success rings, final states and episode statistics, bit for bit; several
     launches in a row (state written back and picked up again).  Small work
-    units (chunk) hand each tile between workgroups several times per launch,
-    and the ring (3) is shorter than a launch, so slots are rewritten by later
-    units that may run on another XCD."""
+    units (chunk) hand each tile between workgroups several times per launch.
+    With a ring (R = 3) shorter than a launch, slots are rewritten by later
+    units that may run on another XCD (full release between units); with
+    R >= the launch, only the state is handed over (write-through, no fence)."""
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 64)
     n = 5000                                   # a partial last tile
     specs = synthetic_specs(pool, W, W, n, 0, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
-    R, chunks = 3, [5, 1, 9]
+    chunks = [5, 1, 9]
     T = sum(chunks)
     rng = np.random.RandomState(4)
     acts = torch.as_tensor(rng.randint(0, 6, size=(T, n)).astype(np.int32), device="cuda")

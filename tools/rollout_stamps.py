@@ -25,7 +25,8 @@ from psketch_amd import CraftSim, sample_scenarios, synthetic_specs  # noqa: E40
 
 lib = _native.lib()
 lib.craft_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-n, R, K = 65536, 16, 32
+n, R = 65536, 16
+K = int(sys.argv[5]) if len(sys.argv) > 5 else 32
 tile = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 store = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 chunk = int(sys.argv[3]) if len(sys.argv) > 3 else 0
