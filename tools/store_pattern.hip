@@ -7,6 +7,7 @@
 // Build (on the GPU box): hipcc --offload-arch=gfx950 -O3 -w -o store_pattern tools/store_pattern.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 typedef unsigned int v4 __attribute__((ext_vector_type(4)));
@@ -27,6 +28,24 @@ __global__ __launch_bounds__(256) void tiles_k(uint8_t* ring, long slot, int R, 
   }
 }
 
+// each wave writes its own contiguous 1/FRONTS of the tile: FRONTS write fronts per workgroup
+template <int TILE, int FRONTS>
+__global__ __launch_bounds__(256) void tiles_fronts(uint8_t* ring, long slot, int R, int K, int row16) {
+  const long base = (long)blockIdx.x * TILE * row16;
+  const int total = TILE * row16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int part = (total + FRONTS - 1) / FRONTS;
+  const int f = wave % FRONTS, waves_per_front = 4 / FRONTS, wf = wave / FRONTS;
+  const int lo = f * part, hi = min(total, lo + part);
+  v4 z = {1u, 2u, 3u, 4u};
+  for (int k = 0; k < K; ++k) {
+    uint8_t* out = ring + (k % R) * slot;
+    for (int s = lo + wf * 64 + lane; s < hi; s += 64 * waves_per_front)
+      *reinterpret_cast<v4*>(out + (base + s) * 16) = z;
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void fill(uint8_t* out, long n16) {
   v4 z = {1u, 2u, 3u, 4u};
   for (long s = blockIdx.x * 256L + threadIdx.x; s < n16; s += (long)gridDim.x * 256)
@@ -41,13 +60,18 @@ int main() {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   std::vector<uint8_t*> rings;
-  const char* names[] = {"tile64", "tile32", "tile128", "tile64_nt", "tile256", "fill"};
+  const char* names[] = {"tile64", "tile32", "tile128", "tile64_nt", "tile256", "fill", "t64_f2", "t64_f4", "t128_f4"};
+  const bool contiguous = getenv("CONTIG") != nullptr;
   for (int i = 0; i < 6; ++i) {
     uint8_t* p;
-    if (hipMalloc(&p, slot * R) != hipSuccess) return 1;
+    if (contiguous) {
+      if (hipExtMallocWithFlags((void**)&p, slot * R, hipDeviceMallocContiguous) != hipSuccess) return 1;
+    } else if (hipMalloc(&p, slot * R) != hipSuccess) {
+      return 1;
+    }
     rings.push_back(p);
     printf("ring %d:", i);
-    for (int mode = 0; mode < 6; ++mode) {
+    for (int mode = 0; mode < 9; ++mode) {
       float ms = 0;
       for (int w = 0; w < 2; ++w) {
         (void)hipEventRecord(a);
@@ -58,7 +82,10 @@ int main() {
             case 2: tiles_k<128, false><<<rows / 128, 256>>>(p, slot, R, K, row16, rows); break;
             case 3: tiles_k<64, true><<<rows / 64, 256>>>(p, slot, R, K, row16, rows); break;
             case 4: tiles_k<256, false><<<rows / 256, 256>>>(p, slot, R, K, row16, rows); break;
-            default: for (int k = 0; k < K; ++k) fill<<<2048, 256>>>(p + (k % R) * slot, slot / 16);
+            case 5: for (int k = 0; k < K; ++k) fill<<<2048, 256>>>(p + (k % R) * slot, slot / 16); break;
+            case 6: tiles_fronts<64, 2><<<rows / 64, 256>>>(p, slot, R, K, row16); break;
+            case 7: tiles_fronts<64, 4><<<rows / 64, 256>>>(p, slot, R, K, row16); break;
+            default: tiles_fronts<128, 4><<<rows / 128, 256>>>(p, slot, R, K, row16); break;
           }
         }
         (void)hipEventRecord(b);
