@@ -261,7 +261,8 @@ int craft_rollout(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed
  * partial sums afterwards. */
 int craft_stats(craft_sim_t* sim, int64_t* stats_out, int32_t reset, void* stream);
 
-/* ---- reference-granular surface (CraftState methods), over slot lists ---- */
+/* ---- reference-granular surface (CraftState methods), over slot lists ----
+ * For every call below, n == 0 is a no-op that returns CRAFT_OK (pointers unused). */
 
 /* CraftState.step (craft.py:332-424) as a pure transition: slot dst[i] becomes
  * step(slot src[i], actions[i]) — src == dst updates in place, src != dst keeps

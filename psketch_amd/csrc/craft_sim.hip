@@ -583,7 +583,9 @@ int craft_stats(craft_sim_t* s, int64_t* stats_out, int32_t reset, void* stream)
 
 int craft_transition(craft_sim_t* s, const int32_t* src, const int32_t* dst, const int32_t* actions,
                      int64_t n, int8_t* code_out, void* stream) {
-  if (!s || !actions || n < 0) return fail(s, CRAFT_EINVAL, "craft_transition: bad argument");
+  if (!s) return CRAFT_EINVAL;
+  if (n == 0) return CRAFT_OK;
+  if (!actions || n < 0) return fail(s, CRAFT_EINVAL, "craft_transition: bad argument");
   if (!src && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_transition: n > n_envs");
   TileArgs a{};
   a.src = src;
@@ -596,7 +598,9 @@ int craft_transition(craft_sim_t* s, const int32_t* src, const int32_t* dst, con
 
 int craft_observe(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t* tasks, void* obs,
                   int8_t* sat, void* stream) {
-  if (!s || n < 0) return fail(s, CRAFT_EINVAL, "craft_observe: bad argument");
+  if (!s) return CRAFT_EINVAL;
+  if (n == 0) return CRAFT_OK;
+  if (n < 0) return fail(s, CRAFT_EINVAL, "craft_observe: bad argument");
   if (!slots && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_observe: n > n_envs");
   if (obs && !aligned16(obs)) return fail(s, CRAFT_EINVAL, "craft_observe: obs must be 16-byte aligned");
   TileArgs a{};
@@ -610,7 +614,9 @@ int craft_observe(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
 
 int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t* tasks, int32_t* action_out,
                   int32_t* path_len_out, void* stream) {
-  if (!s || !action_out || n < 0) return fail(s, CRAFT_EINVAL, "craft_teacher: bad argument");
+  if (!s) return CRAFT_EINVAL;
+  if (n == 0) return CRAFT_OK;
+  if (!action_out || n < 0) return fail(s, CRAFT_EINVAL, "craft_teacher: bad argument");
   if (!slots && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_teacher: n > n_envs");
   if (4 * s->view.C > 1000)
     return fail(s, CRAFT_EINVAL, "craft_teacher: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
@@ -623,7 +629,9 @@ int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
 
 int craft_get_state(craft_sim_t* s, const int32_t* slots, int64_t n, int32_t* agent, int32_t* inventory,
                     uint8_t* grid, int32_t* spec, void* stream) {
-  if (!s || n < 0) return fail(s, CRAFT_EINVAL, "craft_get_state: bad argument");
+  if (!s) return CRAFT_EINVAL;
+  if (n == 0) return CRAFT_OK;
+  if (n < 0) return fail(s, CRAFT_EINVAL, "craft_get_state: bad argument");
   if (!slots && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_get_state: n > n_envs");
   if (n == 0) return CRAFT_OK;
   hipLaunchKernelGGL(craft::get_state_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
@@ -635,7 +643,9 @@ int craft_get_state(craft_sim_t* s, const int32_t* slots, int64_t n, int32_t* ag
 
 int craft_set_state(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t* spec, const int32_t* agent,
                     const int32_t* inventory, void* stream) {
-  if (!s || n < 0 || !spec || !agent) return fail(s, CRAFT_EINVAL, "craft_set_state: bad argument");
+  if (!s) return CRAFT_EINVAL;
+  if (n == 0) return CRAFT_OK;
+  if (n < 0 || !spec || !agent) return fail(s, CRAFT_EINVAL, "craft_set_state: bad argument");
   if (!slots && n > s->n_envs) return fail(s, CRAFT_ERANGE, "craft_set_state: n > n_envs");
   if (n == 0) return CRAFT_OK;
   hipLaunchKernelGGL(craft::set_state_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,

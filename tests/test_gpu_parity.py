@@ -445,3 +445,32 @@ def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, 
     a.check()
     b.check()
     assert host(b.stats())[2] > 0
+
+
+def test_empty_and_single_env_calls(gpu):
+    """Zero-length calls are no-ops (no launch, no error); a one-env simulator
+    runs every entry point."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 4)
+    sim = sim_with_pool(world, 1, pool)
+    e32 = torch.empty(0, dtype=torch.int32, device="cuda")
+    sim.teacher(slots=e32)
+    sim.observe(slots=e32, obs=torch.empty((0, sim.n_features), device="cuda"))
+    sim.transition(e32, src=e32, dst=e32)
+    sim.rollout(0, obs=torch.empty((1, 1, sim.n_features), device="cuda"))
+    sim.generate_pool(0)
+    sim.get_state(slots=e32)
+    sim.check()
+    specs = synthetic_specs(pool, 12, 12, 1, 0, seed=0, task_ids=[t.id for t in tm.dataset_tasks()])
+    obs = sim.empty_obs()
+    sim.reset(*specs, obs=obs)
+    for t in range(45):                                    # crosses an episode boundary
+        sim.step(seed=1, tick=t, obs=obs)
+    ring = torch.empty((4, 1, sim.n_features), device="cuda")
+    sim.rollout(8, seed=1, tick0=45, obs=ring)
+    act, _ = sim.teacher()
+    assert int(act[0]) in range(6)
+    stats = host(sim.stats())
+    assert stats[2] == 53 and stats[1] >= 1
+    sim.check()
