@@ -148,13 +148,16 @@ int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capaci
 int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu,
                    int32_t obs_store);
 
-/* Work-unit length of craft_rollout: the launch is cut into (tile, chunk of
+/* craft_rollout scheduling knobs (results are identical for every setting).
+ * chunk_ticks: work-unit length.  The launch is cut into (tile, chunk of
  * chunk_ticks ticks) units handed out dynamically to the workgroups, a tile's
  * state passing between workgroups at chunk boundaries, so slow workgroups do
  * fewer units.  0 (default) = one unit per tile for the whole launch, which
  * measured fastest at 65536 envs (the balance gained does not pay for the
- * hand-offs).  Results are identical for every setting. */
-int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks);
+ * hand-offs).  threads: threads per tile workgroup, 0 (default) =
+ * 8 per env (7 waves stream a 64-env tile), or 4 per env with 256 / 128
+ * (128, 256 or 512 are accepted; a 16-env tile always runs 128). */
+int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
 /* Element type of every observation buffer this handle writes (craft_reset,
  * craft_step, craft_step_ex, craft_observe).  The features are small

@@ -10,6 +10,8 @@ import torch  # noqa: F401  (load torch's HIP runtime first so the library share
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libpsketch_craft.so")
+# diagnostic builds (tools/) may point at another in-tree build of the same ABI
+LIB_PATH = os.environ.get("PSKETCH_CRAFT_LIB", LIB_PATH)
 
 ABI_VERSION = 1
 MAX_KINDS = 32
@@ -109,7 +111,7 @@ SIGNATURES = {
     "craft_sim_check": (_i32, [_vp, ctypes.POINTER(_i64), _vp]),
     "craft_sim_tune": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
-    "craft_sim_tune_rollout": (_i32, [_vp, _i32]),
+    "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),
     "craft_pool_load": (_i32, [_vp, _vp, _i32, _i32]),
     "craft_pool_generate": (_i32, [_vp, _u64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32,
                                    _vp, _vp]),

@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 
@@ -24,7 +25,6 @@ constexpr int kThreads = 256;      // threads per tile workgroup
 constexpr int kMaxTileEnvs = 64;   // envs per workgroup tile: 16, 32 or 64
 constexpr int kMinTileEnvs = 16;
 constexpr int kInvStride = 36;     // LDS bytes per inventory row (9 dwords: bank-spread)
-constexpr int kRecipeBytes = 12;  // compact recipe: out, ws, n_in, (kind, count) x 4, pad
 
 enum Mode { MODE_TICK = 0, MODE_TRANSITION = 1, MODE_OBSERVE = 2, MODE_RESET = 3 };
 
@@ -45,13 +45,18 @@ struct SimView {
   int32_t obs_policy;         // observation stores: 0 write-back, 1 nontemporal, 2 write-through (sc1)
   int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
-  const uint8_t* rc;          // [CRAFT_MAX_RECIPES][kRecipeBytes] compact recipes
+  // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
+  // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16.  Kernel-argument memory: read with
+  // wave-uniform indices, so they load into scalar registers.
+  uint32_t rcw[CRAFT_MAX_RECIPES * 3];
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
 };
 
 // Dynamic-LDS carve of a tile workgroup (16-byte aligned pieces, Guideline 17):
-// grid rows [tile][GS] | observation bytes [tile * F] (contiguous rows) |
-// inventory rows [tile][36] | task table [64] u16 | recipes [16][12] |
+// grid rows [tile][GS] (the rollout kernel adds the scenario's pristine rows
+// [tile][GS]) | observation bytes [tile * F] (contiguous rows; the rollout
+// kernel double-buffers them, each buffer 16-byte aligned) |
+// inventory rows [tile][36] | task table [64] u16 |
 // agent words [tile] u32.
 #ifdef CRAFT_STAMPS
 // Diagnostic build only (never the product): thread 0 of every workgroup
@@ -77,16 +82,16 @@ struct SimView {
 #endif
 
 struct LdsLayout {
-  int obs, inv, task, rc, agent, ctrl, bytes;
+  int obs, inv, task, agent, ctrl, bytes;
 };
-__host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F) {
+__host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F, int obs_bufs = 1,
+                                                 bool pristine = false) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   LdsLayout l;
-  l.obs = up16(tile * GS);
-  l.inv = up16(l.obs + tile * F);
+  l.obs = up16(tile * GS * (pristine ? 2 : 1));
+  l.inv = up16(l.obs + obs_bufs * up16(tile * F));
   l.task = up16(l.inv + tile * kInvStride);
-  l.rc = up16(l.task + CRAFT_MAX_TASKS * 2);
-  l.agent = up16(l.rc + CRAFT_MAX_RECIPES * kRecipeBytes);
+  l.agent = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.ctrl = up16(l.agent + tile * 4);         // workgroup-uniform control words (rollout queue)
   l.bytes = l.ctrl + 16;
   return l;
@@ -199,7 +204,7 @@ __device__ __forceinline__ void mask_set(uint32_t (&m)[8], int c) {
 }
 
 // CraftState.step (craft.py:332-424) on an LDS grid row `g` and inventory
-// bytes `iv`; `rc_tab` is the compact recipe table (LDS).  Records whether inventory / mask changed.
+// bytes `iv`; the recipes come from v.rcw.  Records whether inventory / mask changed.
 // What PrimitiveLanguageTeacher.describe reads off a (state, next state) pair
 // (teachers/primitive_language.py:61-85): 0..3 = moved by the coord_change of
 // DOWN / UP / LEFT / RIGHT, 4 = did not move and the inventory changed, 5 = neither.
@@ -209,7 +214,7 @@ __device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, b
   return dy < 0 ? CRAFT_DOWN : dy > 0 ? CRAFT_UP : dx < 0 ? CRAFT_LEFT : CRAFT_RIGHT;
 }
 
-__device__ __forceinline__ void transition(const SimView& v, const uint8_t* rc_tab, uint8_t* g, uint8_t* iv, Agent& s,
+__device__ __forceinline__ void transition(const SimView& v, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
                                            bool& mask_changed) {
   const int H = v.H;
@@ -232,18 +237,32 @@ __device__ __forceinline__ void transition(const SimView& v, const uint8_t* rc_t
           g[c] = 0;
           mask_set(m, c);
           inv_changed = mask_changed = true;
+#ifndef CRAFT_ABL_NORECIPE
         } else if (cls == CRAFT_KIND_WORKSHOP) {     // recipes in dict order, craft.py:388-401
+          // Recipe words are wave-uniform kernel-argument words (scalar loads); a recipe's
+          // ingredient counts are read together, so a matching recipe costs two LDS round
+          // trips.  Recipes chain (a product may be the next one's ingredient): each reads
+          // the inventory after the previous one's writes (LDS is in order).
           for (int r = 0; r < v.n_recipes; ++r) {
-            const uint8_t* rc = rc_tab + kRecipeBytes * r;
-            if (rc[1] != thing) continue;
-            const int n_in = rc[2];
-            bool have = true;
-            for (int i = 0; i < n_in; ++i) have = have && iv[rc[3 + 2 * i]] >= rc[4 + 2 * i];
+            const uint32_t a0 = v.rcw[3 * r];
+            if ((int)((a0 >> 8) & 0xff) != thing) continue;     // the recipe's workshop
+            const uint32_t a1 = v.rcw[3 * r + 1], a2 = v.rcw[3 * r + 2];
+            const int n_in = (a0 >> 16) & 0xff;
+            const int k0 = a0 >> 24, k1 = (a1 >> 8) & 0xff, k2 = a1 >> 24, k3 = (a2 >> 8) & 0xff;
+            const int c0 = a1 & 0xff, c1 = (a1 >> 16) & 0xff, c2 = a2 & 0xff, c3 = (a2 >> 16) & 0xff;
+            const int h0 = iv[k0], h1 = iv[k1], h2 = iv[k2], h3 = iv[k3];   // unused slots read kind 0
+            const bool have = (n_in < 1 || h0 >= c0) && (n_in < 2 || h1 >= c1) &&
+                              (n_in < 3 || h2 >= c2) && (n_in < 4 || h3 >= c3);
             if (!have) continue;
-            iv[rc[0]] = (uint8_t)(iv[rc[0]] + 1);    // `_yield` 1 (validated at create)
-            for (int i = 0; i < n_in; ++i) iv[rc[3 + 2 * i]] = (uint8_t)(iv[rc[3 + 2 * i]] - rc[4 + 2 * i]);
+            const int out = a0 & 0xff;
+            iv[out] = (uint8_t)(iv[out] + 1);        // `_yield` 1 (validated at create)
+            if (n_in > 0) iv[k0] = (uint8_t)(iv[k0] - c0);
+            if (n_in > 1) iv[k1] = (uint8_t)(iv[k1] - c1);
+            if (n_in > 2) iv[k2] = (uint8_t)(iv[k2] - c2);
+            if (n_in > 3) iv[k3] = (uint8_t)(iv[k3] - c3);
             inv_changed = true;
           }
+#endif
         } else if (cls == CRAFT_KIND_WATER) {        // craft.py:403-406
           if (iv[v.bridge] > 0) {
             g[c] = 0;

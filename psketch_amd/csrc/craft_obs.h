@@ -148,4 +148,81 @@ __device__ __forceinline__ void scatter_features(const SimView& v, const uint8_t
   }
 }
 
+// Phase D for one env, split over P lanes of the rollout kernel's producer wave
+// (right after the envs' transitions, no workgroup barrier): the features() row
+// (craft.py:296-330) is WIN + 1 items, item 0 = local one-hot + inventory + dir
+// one-hot, item 1 + bi = the pooled blocks of block row bi, and part p of the env
+// writes items p, p + P, ...  `ag` = x | y<<8 | dir<<16; `row` is zeroed.  A
+// block row is built column by column (each of its WIN columns ORs the kind bits
+// of its cells into the WIN blocks it crosses); columns or cells outside the
+// grid are skipped (pad_slice's zero padding, misc/array.py:3-25).
+template <int WIN, int P>
+__device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t* g, const uint8_t* iv,
+                                                 uint32_t ag, uint8_t* row, int part) {
+  const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+  const int W = v.W, H = v.H, K = v.K;
+  constexpr int W2 = WIN * WIN, hw = WIN / 2, bh = W2 / 2;
+  const int L = W2 * K;
+#pragma unroll 1
+  for (int item = part; item <= WIN; item += P) {
+    if (item == 0) {
+      // every read is unconditional (clamped index, result masked), so the compiler issues
+      // them back to back instead of one LDS round trip per predicated cell
+      int kk[WIN * WIN];
+#pragma unroll
+      for (int i = 0; i < WIN; ++i)                                 // local one-hot
+#pragma unroll
+        for (int j = 0; j < WIN; ++j) {
+          const int cx = x - hw + i, cy = y - hw + j;
+          const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+          const int k = g[min(max(cx, 0), W - 1) * H + min(max(cy, 0), H - 1)];
+          kk[i * WIN + j] = ok ? k : 0;
+        }
+#pragma unroll
+      for (int c = 0; c < WIN * WIN; ++c)
+        if (kk[c]) row[c * K + kk[c]] = 1;
+      {                                                             // inventory counts
+        const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);   // 8 independent reads
+        uint32_t w[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w[q] = ivw[q];
+        uint8_t* irow = row + 2 * L;
+#pragma unroll
+        for (int k = 0; k < CRAFT_MAX_KINDS; ++k)
+          if (k < K) irow[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+      }
+      row[2 * L + K + dir] = 1;                                     // dir one-hot
+    } else {
+      const int bi = item - 1;                                      // block-max-pooled one-hots
+      uint32_t m[WIN];
+#pragma unroll
+      for (int bj = 0; bj < WIN; ++bj) m[bj] = 0;
+      const int x0 = x - bh + bi * WIN;
+#pragma unroll
+      for (int ii = 0; ii < WIN; ++ii) {
+        const int cx = x0 + ii;
+        const bool okx = (unsigned)cx < (unsigned)W;
+        const uint8_t* col = g + min(max(cx, 0), W - 1) * H;
+#pragma unroll
+        for (int bj = 0; bj < WIN; ++bj)
+#pragma unroll
+          for (int jj = 0; jj < WIN; ++jj) {
+            const int cy = y - bh + bj * WIN + jj;
+            const uint32_t k = col[min(max(cy, 0), H - 1)];          // unconditional read
+            m[bj] |= (okx && (unsigned)cy < (unsigned)H) ? (1u << k) : 0u;
+          }
+      }
+#pragma unroll
+      for (int bj = 0; bj < WIN; ++bj) {
+        uint32_t msk = m[bj] & ~1u;                                 // kind 0 = empty
+        uint8_t* brow = row + L + (bi * WIN + bj) * K;
+        while (msk) {
+          brow[__ffs(msk) - 1] = 1;
+          msk &= msk - 1;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace craft

@@ -14,7 +14,7 @@ hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const Tile
                        hipStream_t st);
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st);
-hipError_t launch_rollout(int win, int tile, const SimView& v, const RolloutArgs& a, size_t lds,
+hipError_t launch_rollout(int win, int tile, int threads, const SimView& v, const RolloutArgs& a, size_t lds,
                           hipStream_t st);
 hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t st);
 
@@ -132,13 +132,13 @@ struct craft_sim {
   uint4* d_mask = nullptr;
   uint16_t* d_task = nullptr;
   int32_t* d_task_sub = nullptr;
-  uint8_t* d_rc = nullptr;
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   SimView view{};
   int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
   int resident_cap = 0;             // 0: no cap on tile workgroups per CU
   int rollout_chunk = 0;            // craft_rollout ticks per work unit (0: the whole launch)
+  int rollout_threads = 0;          // craft_rollout threads per tile workgroup (0: 8 per env)
   uint8_t* d_sync = nullptr;        // craft_rollout: work-unit counter + per-tile chunk flags
   size_t sync_bytes = 0;
   std::string last_error;
@@ -211,9 +211,9 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // LDS bytes per tile workgroup; a residency cap R pads the request to 160 KiB / R
 // so that at most R tile workgroups share a CU and later tiles' prologues overlap
 // earlier tiles' observation stores.
-size_t lds_bytes(const craft_sim* s, int tile) {
+size_t lds_bytes(const craft_sim* s, int tile, int obs_bufs = 1, bool pristine = false) {
   const SimView& v = s->view;
-  size_t b = (size_t)craft::lds_layout(tile, v.GS, v.F).bytes;
+  size_t b = (size_t)craft::lds_layout(tile, v.GS, v.F, obs_bufs, pristine).bytes;
   if (s->resident_cap > 0) {
     const size_t capped = ((size_t)163840 / s->resident_cap) & ~size_t(15);
     if (capped > b) b = capped;
@@ -269,10 +269,10 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
-  std::vector<uint8_t> rcb(CRAFT_MAX_RECIPES * craft::kRecipeBytes, 0);
+  uint32_t rcw[CRAFT_MAX_RECIPES * 3] = {};          // SimView::rcw packing (craft_device.h)
   for (int r = 0; r < cfg->n_recipes; ++r) {
     const craft_recipe_t& rc = cfg->recipe[r];
-    uint8_t* b = rcb.data() + craft::kRecipeBytes * r;
+    uint8_t b[12] = {};
     b[0] = (uint8_t)rc.output;
     b[1] = (uint8_t)rc.workshop;
     b[2] = (uint8_t)rc.n_inputs;
@@ -280,6 +280,9 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
       b[3 + 2 * i] = (uint8_t)rc.input_kind[i];
       b[4 + 2 * i] = (uint8_t)rc.input_count[i];
     }
+    for (int q = 0; q < 3; ++q)
+      rcw[3 * r + q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) | ((uint32_t)b[4 * q + 2] << 16) |
+                       ((uint32_t)b[4 * q + 3] << 24);
   }
   std::vector<uint16_t> task_tab(CRAFT_MAX_TASKS, 0);
   std::vector<int32_t> task_sub(CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS, 0);
@@ -307,7 +310,6 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_mask, 2 * sizeof(uint4) * n_envs);
   ALLOC(s->d_task, sizeof(uint16_t) * task_tab.size());
   ALLOC(s->d_task_sub, sizeof(int32_t) * task_sub.size());
-  ALLOC(s->d_rc, rcb.size());
   ALLOC(s->d_stats, 4 * sizeof(int64_t) * s->n_tiles);
   ALLOC(s->d_err, 4 * sizeof(int32_t));
   s->sync_bytes = (16 + 4 * (size_t)((n_envs + 15) / 16) + 15) & ~size_t(15);   // queue + tile_done
@@ -315,8 +317,6 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
 #undef ALLOC
   if ((e = hipMemcpy(s->d_task, task_tab.data(), sizeof(uint16_t) * task_tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "task table");
-  if ((e = hipMemcpy(s->d_rc, rcb.data(), rcb.size(), hipMemcpyHostToDevice)) != hipSuccess)
-    return cleanup(e, "recipe table");
   if ((e = hipMemcpy(s->d_task_sub, task_sub.data(), sizeof(int32_t) * task_sub.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "subtask table");
 
@@ -347,7 +347,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     if (k < 16) v.kc_lo |= cls << (4 * k);
     else v.kc_hi |= cls << (4 * (k - 16));
   }
-  v.rc = s->d_rc;
+  for (int q = 0; q < CRAFT_MAX_RECIPES * 3; ++q) v.rcw[q] = rcw[q];
   *out = s;
   return CRAFT_OK;
 }
@@ -367,11 +367,14 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
   return CRAFT_OK;
 }
 
-int craft_sim_tune_rollout(craft_sim_t* s, int32_t chunk_ticks) {
+int craft_sim_tune_rollout(craft_sim_t* s, int32_t chunk_ticks, int32_t threads) {
   if (!s) return CRAFT_EINVAL;
   if (chunk_ticks < 0 || chunk_ticks > 4096)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune_rollout: chunk_ticks must be 0..4096");
+  if (threads != 0 && threads != 128 && threads != 256 && threads != 512)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_rollout: threads must be 0, 128, 256 or 512");
   s->rollout_chunk = chunk_ticks;
+  s->rollout_threads = threads;
   return CRAFT_OK;
 }
 
@@ -393,7 +396,6 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_mask);
   (void)hipFree(s->d_task);
   (void)hipFree(s->d_task_sub);
-  (void)hipFree(s->d_rc);
   (void)hipFree(s->d_stats);
   (void)hipFree(s->d_err);
   (void)hipFree(s->d_sync);
@@ -566,7 +568,7 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   a.tile_done = reinterpret_cast<uint32_t*>(s->d_sync + 16);
   if (n_ticks > 0)
     HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
-  hipError_t e = craft::launch_rollout(s->cfg.window_width, s->tile, s->view, a, lds_bytes(s, s->tile),
+  hipError_t e = craft::launch_rollout(s->cfg.window_width, s->tile, s->rollout_threads, s->view, a, lds_bytes(s, s->tile, 2, true),
                                        reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");
   return CRAFT_OK;

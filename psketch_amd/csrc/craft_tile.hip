@@ -29,7 +29,6 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   uint8_t* s_obs = smem + lay.obs;
   uint8_t* s_inv = smem + lay.inv;
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
-  uint8_t* s_rc = smem + lay.rc;
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
 
   const int tid = threadIdx.x;
@@ -42,8 +41,6 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   // ---- A + C: wave 0, one lane per env ------------------------------------------------------
   if (tid < TILE) {
     for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
-    for (int t = tid; t < CRAFT_MAX_RECIPES * kRecipeBytes / 4; t += TILE)
-      reinterpret_cast<uint32_t*>(s_rc)[t] = reinterpret_cast<const uint32_t*>(v.rc)[t];
 
     int64_t slot = 0, dslot = 0;
     bool live = tid < nE;
@@ -182,7 +179,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
             latch_error(v.err, CRAFT_EBADACTION, slot);
           } else {
             const int ox = s.x, oy = s.y;
-            transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+            transition(v, g, iv, s, m, act, inv_changed, mask_changed);
             code = transition_code(ox, oy, s, inv_changed);
           }
         }
@@ -191,7 +188,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
           latch_error(v.err, CRAFT_EBADACTION, slot);
         } else if (act >= 0) {
           const int ox = s.x, oy = s.y;
-          transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+          transition(v, g, iv, s, m, act, inv_changed, mask_changed);
           code = transition_code(ox, oy, s, inv_changed);
         }
         if (dslot != slot) inv_changed = mask_changed = true;   // copy-on-step

@@ -80,10 +80,12 @@ class CraftSim:
         self._check(N.lib().craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu),
                                            int(obs_store)), "craft_sim_tune")
 
-    def tune_rollout(self, chunk_ticks=0):
+    def tune_rollout(self, chunk_ticks=0, threads=0):
         """Ticks per dynamically scheduled work unit of rollout() (0 = the whole
-        launch, the default); results are identical for every setting."""
-        self._check(N.lib().craft_sim_tune_rollout(self._h, int(chunk_ticks)), "craft_sim_tune_rollout")
+        launch, the default) and threads per tile workgroup (0 = 8 per env);
+        results are identical for every setting."""
+        self._check(N.lib().craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
+                    "craft_sim_tune_rollout")
 
     _OBS_FORMATS = {"f32": (N.OBS_F32, torch.float32), "bf16": (N.OBS_BF16, torch.bfloat16),
                     "u8": (N.OBS_U8, torch.uint8)}

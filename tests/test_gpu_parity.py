@@ -386,20 +386,29 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
     sim.check()
 
 
-@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given,chunk,R", [
-    ("craft_medium_12x12", 12, 0, "f32", True, False, 0, 3),
-    ("craft_medium_12x12", 12, 0, "f32", True, False, 1, 3),
-    ("craft_medium_12x12", 12, 0, "f32", True, False, 1, 16),
-    ("craft_medium_12x12", 12, 16, "bf16", True, True, 2, 3),
-    ("craft_medium_12x12", 12, 32, "u8", False, True, 3, 16),
-    ("craft_medium_12x12_w5", 12, 0, "f32", True, False, 2, 3),
-    ("craft_16x16_w7", 16, 0, "f32", False, False, 0, 3),
-    ("craft_medium", 8, 64, "f32", True, True, 1, 9)])
-def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, chunk, R):
+@pytest.mark.parametrize("world,W,tile,fmt,autoreset,given,chunk,R,threads", [
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 0, 3, 0),
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 0, 16, 256),
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 1, 3, 0),
+    ("craft_medium_12x12", 12, 0, "f32", True, False, 1, 16, 0),
+    ("craft_medium_12x12", 12, 0, "bf16", True, False, 2, 16, 256),
+    ("craft_medium_12x12", 12, 16, "bf16", True, True, 2, 3, 0),
+    ("craft_medium_12x12", 12, 32, "u8", False, True, 3, 16, 0),
+    ("craft_medium_12x12", 12, 32, "f32", True, True, 0, 16, 128),
+    ("craft_medium_12x12", 12, 32, "f32", True, False, 1, 3, 512),
+    ("craft_medium_12x12", 12, 16, "f32", True, False, 0, 16, 256),
+    ("craft_medium_12x12_w5", 12, 0, "f32", True, False, 2, 3, 0),
+    ("craft_medium_12x12_w5", 12, 0, "u8", True, False, 0, 3, 128),
+    ("craft_16x16_w7", 16, 0, "f32", False, False, 0, 3, 0),
+    ("craft_16x16_w7", 16, 32, "f32", True, False, 0, 3, 256),
+    ("craft_medium", 8, 64, "f32", True, True, 1, 9, 0),
+    ("craft_medium", 8, 64, "f32", True, True, 0, 9, 256)])
+def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, chunk, R, threads):
     """craft_rollout(K ticks) == K craft_step calls: observation / reward / done /
     success rings, final states and episode statistics, bit for bit; several
     launches in a row (state written back and picked up again).  Small work
     units (chunk) hand each tile between workgroups several times per launch.
+    Every workgroup width (2 to 16 threads per env) is covered.
     With a ring (R = 3) shorter than a launch, slots are rewritten by later
     units that may run on another XCD (full release between units); with
     R >= the launch, only the state is handed over (write-through, no fence)."""
@@ -415,7 +424,7 @@ def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, 
     for _ in range(2):
         sim = sim_with_pool(world, n, pool)
         sim.tune(tile, 0, 1)
-        sim.tune_rollout(chunk)
+        sim.tune_rollout(chunk, threads)
         sim.set_obs_format(fmt)
         sim.reset(*specs)
         sims.append(sim)
