@@ -212,7 +212,9 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
       ag = (uint32_t)__shfl((int)ag, tid % TILE, 64);
     }
     const int e = tid % TILE;
+#ifndef CRAFT_ABL_NOD
     if (ag) scatter_env_part<WIN, P>(v, s_grid + e * v.GS, s_inv + e * kInvStride, ag, buf + e * F, tid / TILE);
+#endif
   };
 
   // ---- once per workgroup: static tables, cleared observation rows ------------------------------

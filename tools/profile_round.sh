@@ -7,7 +7,7 @@ OUT="$REPO/gpurun_out/${TAG:-prof}"
 mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
-ARGS="--steps ${STEPS:-1024} --warmup 64 --no-cpu-baseline ${BENCH_ARGS:-}"
+ARGS="--steps ${STEPS:-1024} --warmup 64 ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 "$REPO/bench.py" $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
