@@ -63,6 +63,8 @@ def parse():
                         "1: one craft_step launch per tick")
     p.add_argument("--rollout-threads", type=int, default=0,
                    help="craft_rollout threads per tile workgroup (0 = 8 per env: 7 streaming waves)")
+    p.add_argument("--rollout-chunk", type=int, default=0,
+                   help="craft_rollout ticks per dynamically scheduled work unit (0 = the whole launch)")
     p.add_argument("--obs-only", action="store_true",
                    help="diagnostic: skip the reward/done/success rings (not a bench line)")
     p.add_argument("--seed", type=int, default=0)
@@ -124,7 +126,7 @@ def main():
     K = max(1, args.ticks_per_launch)
     obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 0)
     sim.tune(args.tile, 0, obs_store)
-    sim.tune_rollout(0, args.rollout_threads)
+    sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
     specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
                             task_ids=tasks)
@@ -224,7 +226,8 @@ def main():
                        "n_features": F, "obs_dtype": "fp32", "obs_ring": args.ring,
                        "pool": args.pool, "parallelism": f"env-shard x{world_size}",
                        "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
-                       "tile": tile, "rollout_threads": args.rollout_threads or 8 * tile, "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]},
+                       "tile": tile, "rollout_threads": args.rollout_threads or 8 * tile,
+                       "rollout_chunk": args.rollout_chunk or K, "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": (f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, {tile}>"

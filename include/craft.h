@@ -156,7 +156,7 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * measured fastest at 65536 envs (the balance gained does not pay for the
  * hand-offs).  threads: threads per tile workgroup, 0 (default) =
  * 8 per env (7 waves stream a 64-env tile), or 4 per env with 256 / 128
- * (128, 256 or 512 are accepted; a 16-env tile always runs 128). */
+ * (128, 256 or 512 are accepted). */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
 /* Element type of every observation buffer this handle writes (craft_reset,

@@ -58,8 +58,13 @@ __device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t en
     for (int u = 0; u < U; ++u) {
       const int sidx = base + u * NTHR;
       if (sidx < nv) {
+#ifdef CRAFT_ABL_NOLDS
+        o[u] = obs_vec{(unsigned)sidx, 0u, 0u, 0u};
+        if (false) {
+#else
         o[u] = pack16<FMT>(s_obs, sidx);
         if (ZERO) {
+#endif
           if (FMT == CRAFT_OBS_F32) reinterpret_cast<uint32_t*>(s_obs)[sidx] = 0u;
           else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint2*>(s_obs)[sidx] = make_uint2(0u, 0u);
           else reinterpret_cast<uint4*>(s_obs)[sidx] = make_uint4(0u, 0u, 0u, 0u);

@@ -346,8 +346,12 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         const unsigned long long t0 = CRAFT_NOW();
         const int64_t r = (a.tick0 + k) % a.ring;
         void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
+#ifndef CRAFT_ABL_NOE
         stream_obs<FMT, NT - 64, true>(s_obs + ((k - k0) & 1) * obs_buf, out, env0, F, nE,
                                        v.obs_policy, et);
+#else
+        (void)out;
+#endif
         const unsigned long long t1 = CRAFT_NOW();
         PACC(4, t1 - t0);
         __syncthreads();
