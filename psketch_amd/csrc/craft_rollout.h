@@ -123,7 +123,11 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         act = a.actions[(int64_t)k * n + slot];
       } else {
         const uint64_t gid = (uint64_t)(v.env_base + slot);
+#ifdef CRAFT_ABL_NOHASH
+        act = (int)((gid + (uint64_t)tick) % 6u);
+#else
         act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)tick) >> 32) % 6u);
+#endif
       }
       bool restart = false;
       if (s.frozen) {
@@ -134,7 +138,11 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         d = (act == CRAFT_STOP) || s.timer <= 0;
         restart = d && (a.flags & CRAFT_STEP_AUTORESET);
       }
+#ifdef CRAFT_ABL_NOSAT
+      if (false) {
+#else
       if (d) {
+#endif
         // satisfies() of the pre-step state (the LDS row already has this episode's clears)
         const int goal = task_word & 0xf, arg = (task_word >> 4) & 0xff;
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));
@@ -177,8 +185,10 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         bool inv_changed = false, mask_changed = false;
         uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // the LDS row is the record
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
+#ifndef CRAFT_ABL_NOTRANS
         if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
         else transition(v, g, iv, s, m_unused, act, inv_changed, mask_changed);
+#endif
         if (mask_changed) {
           const uint32_t nc = (clr >> 24) & 3;
           clr = nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)fc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
