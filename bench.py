@@ -194,7 +194,12 @@ def main():
         total_steps = n * world_size * args.steps
         value = total_steps / elapsed
         bps = bytes_per_env_step(sim.width, sim.height, sim.params["WINDOW_WIDTH"], F)
-        tile = args.tile or {3: 64, 5: 32}.get(sim.params["WINDOW_WIDTH"], 16)
+        win = sim.params["WINDOW_WIDTH"]
+        if K > 1 and not args.rollout_threads and win == 3:
+            tile, threads = 32, 384                      # craft_rollout's default shape (split producer)
+        else:
+            tile = args.tile or {3: 64, 5: 32}.get(win, 16)
+            threads = args.rollout_threads or 8 * tile
         achieved = bps * n * K / (kernel_ms * 1e-3) / 1e9
         traffic = None
         workload = f"{args.world}_w{sim.params['WINDOW_WIDTH']}_B{n}_random_rollout_full_features"
@@ -226,13 +231,14 @@ def main():
                        "n_features": F, "obs_dtype": "fp32", "obs_ring": args.ring,
                        "pool": args.pool, "parallelism": f"env-shard x{world_size}",
                        "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
-                       "tile": tile, "rollout_threads": args.rollout_threads or 8 * tile,
+                       "tile": tile, "rollout_threads": threads,
                        "rollout_chunk": args.rollout_chunk or K, "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": (f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, {tile}>"
                                     if K == 1 else
-                                    f"rollout_kernel<{sim.params['WINDOW_WIDTH']}, {tile}>"),
+                                    (f"rollout_split_kernel<{win}, {tile}, {threads}>" if threads in (320, 384)
+                                     else f"rollout_kernel<{win}, {tile}, {threads}>")),
                          "kernel_us": kernel_ms * 1e3, "ticks_per_launch": K,
                          "bytes_per_launch": bps * n * K, "bytes_per_env_step": bps},
             "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},

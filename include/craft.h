@@ -154,9 +154,12 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * state passing between workgroups at chunk boundaries, so slow workgroups do
  * fewer units.  0 (default) = one unit per tile for the whole launch, which
  * measured fastest at 65536 envs (the balance gained does not pay for the
- * hand-offs).  threads: threads per tile workgroup, 0 (default) =
- * 8 per env (7 waves stream a 64-env tile), or 4 per env with 256 / 128
- * (128, 256 or 512 are accepted). */
+ * hand-offs).  threads: threads per tile workgroup on the tile
+ * set by craft_sim_tune: 128, 256 or 512 (one producer wave, the rest stream),
+ * or, for 16- and 32-env tiles, 320 / 384 for the split-producer kernel
+ * (transition and scatter on two waves, 3 or 4 streaming waves).  0 (default)
+ * = the measured best: 32-env tiles x 384 threads (split) for 3x3 windows,
+ * else the handle's tile with 8 threads per env. */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
 /* Element type of every observation buffer this handle writes (craft_reset,

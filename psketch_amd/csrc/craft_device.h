@@ -21,6 +21,9 @@
 
 namespace craft {
 
+typedef __attribute__((address_space(1))) uint32_t gu32;      // global-memory words for
+typedef __attribute__((address_space(1))) unsigned long long gu64;   // scoped atomics
+
 constexpr int kThreads = 256;      // threads per tile workgroup
 constexpr int kMaxTileEnvs = 64;   // envs per workgroup tile: 16, 32 or 64
 constexpr int kMinTileEnvs = 16;
@@ -46,9 +49,9 @@ struct SimView {
   int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
-  // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16.  Kernel-argument memory: read with
-  // wave-uniform indices, so they load into scalar registers.
-  uint32_t rcw[CRAFT_MAX_RECIPES * 3];
+  // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16.  Kernels copy the table to LDS.
+  // (As kernel-argument words they cost ~50 scalar registers, which spilled.)
+  const uint32_t* rcw;
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
 };
 
@@ -56,7 +59,7 @@ struct SimView {
 // grid rows [tile][GS] (the rollout kernel adds the scenario's pristine rows
 // [tile][GS]) | observation bytes [tile * F] (contiguous rows; the rollout
 // kernel double-buffers them, each buffer 16-byte aligned) |
-// inventory rows [tile][36] | task table [64] u16 |
+// inventory rows [tile][36] | task table [64] u16 | recipe words [16][3] |
 // agent words [tile] u32.
 #ifdef CRAFT_STAMPS
 // Diagnostic build only (never the product): thread 0 of every workgroup
@@ -82,7 +85,7 @@ struct SimView {
 #endif
 
 struct LdsLayout {
-  int obs, inv, task, agent, ctrl, bytes;
+  int obs, inv, task, rc, agent, ctrl, bytes;
 };
 __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F, int obs_bufs = 1,
                                                  bool pristine = false) {
@@ -91,7 +94,8 @@ __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F, int obs
   l.obs = up16(tile * GS * (pristine ? 2 : 1));
   l.inv = up16(l.obs + obs_bufs * up16(tile * F));
   l.task = up16(l.inv + tile * kInvStride);
-  l.agent = up16(l.task + CRAFT_MAX_TASKS * 2);
+  l.rc = up16(l.task + CRAFT_MAX_TASKS * 2);
+  l.agent = up16(l.rc + CRAFT_MAX_RECIPES * 12);
   l.ctrl = up16(l.agent + tile * 4);         // workgroup-uniform control words (rollout queue)
   l.bytes = l.ctrl + 16;
   return l;
@@ -204,7 +208,7 @@ __device__ __forceinline__ void mask_set(uint32_t (&m)[8], int c) {
 }
 
 // CraftState.step (craft.py:332-424) on an LDS grid row `g` and inventory
-// bytes `iv`; the recipes come from v.rcw.  Records whether inventory / mask changed.
+// bytes `iv`; `rc` is the recipe table (LDS copy of v.rcw).  Records whether inventory / mask changed.
 // What PrimitiveLanguageTeacher.describe reads off a (state, next state) pair
 // (teachers/primitive_language.py:61-85): 0..3 = moved by the coord_change of
 // DOWN / UP / LEFT / RIGHT, 4 = did not move and the inventory changed, 5 = neither.
@@ -214,7 +218,7 @@ __device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, b
   return dy < 0 ? CRAFT_DOWN : dy > 0 ? CRAFT_UP : dx < 0 ? CRAFT_LEFT : CRAFT_RIGHT;
 }
 
-__device__ __forceinline__ void transition(const SimView& v, uint8_t* g, uint8_t* iv, Agent& s,
+__device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
                                            bool& mask_changed) {
   const int H = v.H;
@@ -239,14 +243,15 @@ __device__ __forceinline__ void transition(const SimView& v, uint8_t* g, uint8_t
           inv_changed = mask_changed = true;
 #ifndef CRAFT_ABL_NORECIPE
         } else if (cls == CRAFT_KIND_WORKSHOP) {     // recipes in dict order, craft.py:388-401
-          // Recipe words are wave-uniform kernel-argument words (scalar loads); a recipe's
-          // ingredient counts are read together, so a matching recipe costs two LDS round
-          // trips.  Recipes chain (a product may be the next one's ingredient): each reads
+          // Recipe words are wave-uniform (LDS broadcast reads, kept in scalar registers); a
+          // recipe's ingredient counts are read together, so a matching recipe costs two LDS
+          // round trips.  Recipes chain (a product may be the next one's ingredient): each reads
           // the inventory after the previous one's writes (LDS is in order).
           for (int r = 0; r < v.n_recipes; ++r) {
-            const uint32_t a0 = v.rcw[3 * r];
+            const uint32_t a0 = __builtin_amdgcn_readfirstlane(rc[3 * r]);
             if ((int)((a0 >> 8) & 0xff) != thing) continue;     // the recipe's workshop
-            const uint32_t a1 = v.rcw[3 * r + 1], a2 = v.rcw[3 * r + 2];
+            const uint32_t a1 = __builtin_amdgcn_readfirstlane(rc[3 * r + 1]);
+            const uint32_t a2 = __builtin_amdgcn_readfirstlane(rc[3 * r + 2]);
             const int n_in = (a0 >> 16) & 0xff;
             const int k0 = a0 >> 24, k1 = (a1 >> 8) & 0xff, k2 = a1 >> 24, k3 = (a2 >> 8) & 0xff;
             const int c0 = a1 & 0xff, c1 = (a1 >> 16) & 0xff, c2 = a2 & 0xff, c3 = (a2 >> 16) & 0xff;

@@ -32,11 +32,13 @@
 // observations (random rollouts, configs 2 and 4; or replayed action tables).
 #pragma once
 #include "craft_obs.h"
+#include "craft_rollout_split.h"
+
+#ifndef CRAFT_SPLIT_WPE
+#define CRAFT_SPLIT_WPE 4
+#endif
 
 namespace craft {
-
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 // NT threads per workgroup.  Wave 0 is the producer: lanes < TILE own one env
 // each and run its transition C(k+1); then all 64 lanes scatter the tile's
@@ -60,6 +62,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
   const int obs_buf = (TILE * v.F + 15) & ~15;
   uint8_t* s_inv = smem + lay.inv;
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
+  uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   uint32_t* s_ctrl = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
 
   STAMP(0);
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
 #ifndef CRAFT_ABL_NOTRANS
         if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-        else transition(v, g, iv, s, m_unused, act, inv_changed, mask_changed);
+        else transition(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed);
 #endif
         if (mask_changed) {
           const uint32_t nc = (clr >> 24) & 3;
@@ -230,6 +233,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
   // ---- once per workgroup: static tables, cleared observation rows ------------------------------
   if (tid < TILE) {
     for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
+    for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += TILE) s_rc[t] = v.rcw[t];
   }
   if (want_obs) {
     uint4* z = reinterpret_cast<uint4*>(s_obs);
@@ -483,6 +487,51 @@ static hipError_t launch_rollout_one(const SimView& v, const RolloutArgs& a, siz
   return hipGetLastError();
 }
 
+// The split-producer kernel (craft_rollout_split.h) for 16- and 32-env tiles: NT threads =
+// C wave + D wave + NT / 64 - 2 streaming waves, 5 waves per SIMD.
+template <int WIN, int TILE, int NT, int FMT, bool GIVEN>
+static hipError_t launch_rollout_split_one(const SimView& v, const RolloutArgs& a, hipStream_t st) {
+  const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
+  if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
+  constexpr int WPE = WIN == 3 ? CRAFT_SPLIT_WPE : 2;
+  const size_t lds = (size_t)split_lds_bytes(TILE, v.GS, v.F);
+  auto kern = rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  static int resident = 0;
+  static size_t resident_lds = 0;
+  if (resident == 0 || resident_lds != lds) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    resident = per_cu * cus;
+    resident_lds = lds;
+  }
+  const int64_t units = tiles * (int64_t)((a.n_ticks + a.chunk - 1) / a.chunk);
+  const int64_t rounds = (units + resident - 1) / resident;
+  const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;
+  const int64_t grid = std::min<int64_t>((units + rounds - 1) / rounds, rows);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, v, a);
+  return hipGetLastError();
+}
+
+template <int WIN, int TILE, int NT>
+static hipError_t launch_rollout_split(const SimView& v, const RolloutArgs& a, hipStream_t st) {
+  const bool given = a.actions != nullptr;
+  switch (v.obs_fmt) {
+    case CRAFT_OBS_BF16: return given ? launch_rollout_split_one<WIN, TILE, NT, CRAFT_OBS_BF16, true>(v, a, st)
+                                      : launch_rollout_split_one<WIN, TILE, NT, CRAFT_OBS_BF16, false>(v, a, st);
+    case CRAFT_OBS_U8: return given ? launch_rollout_split_one<WIN, TILE, NT, CRAFT_OBS_U8, true>(v, a, st)
+                                    : launch_rollout_split_one<WIN, TILE, NT, CRAFT_OBS_U8, false>(v, a, st);
+    default: return given ? launch_rollout_split_one<WIN, TILE, NT, CRAFT_OBS_F32, true>(v, a, st)
+                          : launch_rollout_split_one<WIN, TILE, NT, CRAFT_OBS_F32, false>(v, a, st);
+  }
+}
+
 template <int WIN, int TILE, int NT>
 static hipError_t launch_rollout_fmt(const SimView& v, const RolloutArgs& a, size_t lds, hipStream_t st) {
   const bool given = a.actions != nullptr;
@@ -502,8 +551,12 @@ static hipError_t launch_rollout_win(int tile, int threads, const SimView& v, co
                                      size_t lds, hipStream_t st) {
   switch (tile) {
     case 16: return threads == 128 ? launch_rollout_fmt<WIN, 16, 128>(v, a, lds, st)
+                  : threads == 320 ? launch_rollout_split<WIN, 16, 320>(v, a, st)
+                  : threads == 384 ? launch_rollout_split<WIN, 16, 384>(v, a, st)
                                    : launch_rollout_fmt<WIN, 16, 256>(v, a, lds, st);
     case 32: return threads == 128 ? launch_rollout_fmt<WIN, 32, 128>(v, a, lds, st)
+                  : threads == 320 ? launch_rollout_split<WIN, 32, 320>(v, a, st)
+                  : threads == 384 ? launch_rollout_split<WIN, 32, 384>(v, a, st)
                   : threads == 512 ? launch_rollout_fmt<WIN, 32, 512>(v, a, lds, st)
                                    : launch_rollout_fmt<WIN, 32, 256>(v, a, lds, st);
     default: return threads == 256 ? launch_rollout_fmt<WIN, 64, 256>(v, a, lds, st)

@@ -29,6 +29,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   uint8_t* s_obs = smem + lay.obs;
   uint8_t* s_inv = smem + lay.inv;
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
+  uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
 
   const int tid = threadIdx.x;
@@ -41,6 +42,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
   // ---- A + C: wave 0, one lane per env ------------------------------------------------------
   if (tid < TILE) {
     for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
+    for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += TILE) s_rc[t] = v.rcw[t];
 
     int64_t slot = 0, dslot = 0;
     bool live = tid < nE;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
             latch_error(v.err, CRAFT_EBADACTION, slot);
           } else {
             const int ox = s.x, oy = s.y;
-            transition(v, g, iv, s, m, act, inv_changed, mask_changed);
+            transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
             code = transition_code(ox, oy, s, inv_changed);
           }
         }
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void tile_kernel(SimView v, TileArgs a) {
           latch_error(v.err, CRAFT_EBADACTION, slot);
         } else if (act >= 0) {
           const int ox = s.x, oy = s.y;
-          transition(v, g, iv, s, m, act, inv_changed, mask_changed);
+          transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
           code = transition_code(ox, oy, s, inv_changed);
         }
         if (dslot != slot) inv_changed = mask_changed = true;   // copy-on-step

@@ -397,6 +397,13 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
     ("craft_medium_12x12", 12, 32, "f32", True, True, 0, 16, 128),
     ("craft_medium_12x12", 12, 32, "f32", True, False, 1, 3, 512),
     ("craft_medium_12x12", 12, 16, "f32", True, False, 0, 16, 256),
+    ("craft_medium_12x12", 12, 16, "f32", True, False, 0, 16, 320),
+    ("craft_medium_12x12", 12, 16, "u8", True, True, 2, 3, 384),
+    ("craft_medium_12x12", 12, 32, "bf16", True, False, 1, 16, 320),
+    ("craft_medium_12x12", 12, 32, "f32", False, False, 0, 3, 384),
+    ("craft_medium_12x12_w5", 12, 16, "f32", True, False, 0, 3, 320),
+    ("craft_16x16_w7", 16, 16, "f32", True, True, 3, 16, 384),
+    ("craft_medium", 8, 16, "f32", True, False, 1, 9, 320),
     ("craft_medium_12x12_w5", 12, 0, "f32", True, False, 2, 3, 0),
     ("craft_medium_12x12_w5", 12, 0, "u8", True, False, 0, 3, 128),
     ("craft_16x16_w7", 16, 0, "f32", False, False, 0, 3, 0),
@@ -408,7 +415,8 @@ def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, 
     success rings, final states and episode statistics, bit for bit; several
     launches in a row (state written back and picked up again).  Small work
     units (chunk) hand each tile between workgroups several times per launch.
-    Every workgroup width (2 to 16 threads per env) is covered.
+    Every workgroup width (2 to 16 threads per env) is covered, and the
+    split-producer kernel (320 / 384 threads on 16- and 32-env tiles).
     With a ring (R = 3) shorter than a launch, slots are rewritten by later
     units that may run on another XCD (full release between units); with
     R >= the launch, only the state is handed over (write-through, no fence)."""
