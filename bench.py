@@ -196,7 +196,7 @@ def main():
         bps = bytes_per_env_step(sim.width, sim.height, sim.params["WINDOW_WIDTH"], F)
         win = sim.params["WINDOW_WIDTH"]
         if K > 1 and not args.rollout_threads and win == 3:
-            tile, threads = 32, 384                      # craft_rollout's default shape (split producer)
+            tile, threads = 32, 512                      # craft_rollout's default shape (split producer)
         else:
             tile = args.tile or {3: 64, 5: 32}.get(win, 16)
             threads = args.rollout_threads or 8 * tile
@@ -237,7 +237,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": (f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, {tile}>"
                                     if K == 1 else
-                                    (f"rollout_split_kernel<{win}, {tile}, {threads}>" if threads in (320, 384)
+                                    (f"rollout_split_kernel<{win}, {tile}, {threads}>"
+                                     if tile <= 32 and threads >= 320
                                      else f"rollout_kernel<{win}, {tile}, {threads}>")),
                          "kernel_us": kernel_ms * 1e3, "ticks_per_launch": K,
                          "bytes_per_launch": bps * n * K, "bytes_per_env_step": bps},

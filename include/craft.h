@@ -155,11 +155,11 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * fewer units.  0 (default) = one unit per tile for the whole launch, which
  * measured fastest at 65536 envs (the balance gained does not pay for the
  * hand-offs).  threads: threads per tile workgroup on the tile
- * set by craft_sim_tune: 128, 256 or 512 (one producer wave, the rest stream),
- * or, for 16- and 32-env tiles, 320 / 384 for the split-producer kernel
- * (transition and scatter on two waves, 3 or 4 streaming waves).  0 (default)
- * = the measured best: 32-env tiles x 384 threads (split) for 3x3 windows,
- * else the handle's tile with 8 threads per env. */
+ * set by craft_sim_tune.  128 or 256: one producer wave, the rest stream; 64-env
+ * tiles also take 512.  16- and 32-env tiles with 320, 384 or 512: the
+ * split-producer kernel (transition and scatter on two waves, the other 3-6
+ * stream).  0 (default) = the measured best: 32-env tiles x 512 threads (split)
+ * for 3x3 windows, else the handle's tile with 8 threads per env. */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
 /* Element type of every observation buffer this handle writes (craft_reset,

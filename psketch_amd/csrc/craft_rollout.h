@@ -34,9 +34,6 @@
 #include "craft_obs.h"
 #include "craft_rollout_split.h"
 
-#ifndef CRAFT_SPLIT16_NT   // diagnostic builds: the 16-env split shape behind threads = 320
-#define CRAFT_SPLIT16_NT 320
-#endif
 #ifndef CRAFT_SPLIT_WPE
 #define CRAFT_SPLIT_WPE 4
 #endif
@@ -554,13 +551,14 @@ static hipError_t launch_rollout_win(int tile, int threads, const SimView& v, co
                                      size_t lds, hipStream_t st) {
   switch (tile) {
     case 16: return threads == 128 ? launch_rollout_fmt<WIN, 16, 128>(v, a, lds, st)
-                  : threads == 320 ? launch_rollout_split<WIN, 16, CRAFT_SPLIT16_NT>(v, a, st)
+                  : threads == 320 ? launch_rollout_split<WIN, 16, 320>(v, a, st)
                   : threads == 384 ? launch_rollout_split<WIN, 16, 384>(v, a, st)
+                  : threads == 512 ? launch_rollout_split<WIN, 16, 512>(v, a, st)
                                    : launch_rollout_fmt<WIN, 16, 256>(v, a, lds, st);
     case 32: return threads == 128 ? launch_rollout_fmt<WIN, 32, 128>(v, a, lds, st)
                   : threads == 320 ? launch_rollout_split<WIN, 32, 320>(v, a, st)
                   : threads == 384 ? launch_rollout_split<WIN, 32, 384>(v, a, st)
-                  : threads == 512 ? launch_rollout_fmt<WIN, 32, 512>(v, a, lds, st)
+                  : threads == 512 ? launch_rollout_split<WIN, 32, 512>(v, a, st)
                                    : launch_rollout_fmt<WIN, 32, 256>(v, a, lds, st);
     default: return threads == 256 ? launch_rollout_fmt<WIN, 64, 256>(v, a, lds, st)
                                    : launch_rollout_fmt<WIN, 64, 512>(v, a, lds, st);

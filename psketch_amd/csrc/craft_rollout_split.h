@@ -157,8 +157,10 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
         bool inv_changed = false, mask_changed = false;
         uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
+#ifndef CRAFT_ABL_NOTRANS
         if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
         else transition(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed);
+#endif
         if (mask_changed) {
           chg = 1u + (uint32_t)fc;
           const uint32_t nc = (clr >> 24) & 3;
@@ -186,7 +188,11 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   auto scatter_d = [&](int q, int nE) {
     const int l = tid - 64, e = l % TILE;
     const uint32_t ag = s_agent[(q & 1) * TILE + e];
+#ifdef CRAFT_ABL_NOD
+    if (false)
+#else
     if (e < nE && ag)
+#endif
       scatter_env_part<WIN, P>(v, s_grid + (q & 1) * TILE * GS + e * GS,
                                s_inv + (q & 1) * TILE * kInvStride + e * kInvStride, ag,
                                s_obs + (q & 1) * obs_buf + e * F, l / TILE);
@@ -321,8 +327,12 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
             const int q = i - 1;
             const int64_t r = (a.tick0 + k0 + q) % a.ring;
             void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
+#ifndef CRAFT_ABL_NOE
             stream_obs<FMT, NT - 128, true>(s_obs + (q & 1) * obs_buf, out, env0, F, nE,
                                             v.obs_policy, et);
+#else
+            (void)out;
+#endif
           }
           __syncthreads();
         }

@@ -574,11 +574,12 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   if (n_ticks > 0)
     HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
   // default shape (threads 0): for 3x3 windows the split-producer kernel on 32-env tiles
-  // (~7 % faster than 64-env tiles at 65536 envs); otherwise the handle's tile
+  // with 6 streaming waves (7-15 % faster than 64-env tiles at 65536 envs);
+  // otherwise the handle's tile
   int tile = s->tile, threads = s->rollout_threads;
   if (threads == 0 && s->cfg.window_width == 3) {
     tile = 32;
-    threads = 384;
+    threads = 512;
   }
   hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, s->view, a, lds_bytes(s, tile, 2, true),
                                        reinterpret_cast<hipStream_t>(stream));

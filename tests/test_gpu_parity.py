@@ -396,6 +396,7 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
     ("craft_medium_12x12", 12, 32, "u8", False, True, 3, 16, 0),
     ("craft_medium_12x12", 12, 32, "f32", True, True, 0, 16, 128),
     ("craft_medium_12x12", 12, 32, "f32", True, False, 1, 3, 512),
+    ("craft_medium_12x12", 12, 16, "bf16", False, True, 0, 16, 512),
     ("craft_medium_12x12", 12, 16, "f32", True, False, 0, 16, 256),
     ("craft_medium_12x12", 12, 16, "f32", True, False, 0, 16, 320),
     ("craft_medium_12x12", 12, 16, "u8", True, True, 2, 3, 384),
@@ -416,7 +417,7 @@ def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, 
     launches in a row (state written back and picked up again).  Small work
     units (chunk) hand each tile between workgroups several times per launch.
     Every workgroup width (2 to 16 threads per env) is covered, and the
-    split-producer kernel (320 / 384 threads on 16- and 32-env tiles).
+    split-producer kernel (320 / 384 / 512 threads on 16- and 32-env tiles).
     With a ring (R = 3) shorter than a launch, slots are rewritten by later
     units that may run on another XCD (full release between units); with
     R >= the launch, only the state is handed over (write-through, no fence)."""

@@ -16,7 +16,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 R = 16
 ring = torch.empty((R, n, 404), dtype=torch.float32, device="cuda")
-for tile, threads in [(64, 512), (64, 256), (32, 256), (32, 512), (16, 256), (16, 128)]:
+for tile, threads in [(32, 384), (64, 512), (32, 256), (16, 256), (16, 320)]:
     sim = CraftSim("craft_medium_12x12", n_envs=n, device=0, pool_capacity=1024)
     g, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, 1024)
     sim.load_pool(g)
