@@ -1,0 +1,405 @@
+// craft_rollout_split.h — craft_rollout for 16- and 32-env tiles: the producer
+// work of a tick split over two waves.
+//
+// Small tiles store faster (store-pattern tables: 16-row tiles reach
+// ~15 us per tick against ~18.5 for 64-row tiles), but every tile needs its own
+// transition latency chain, so one wave doing both the transition and the
+// scatter cannot keep up.  Here:
+//   wave 0        C(q+1): the transitions (one lane per env);
+//   wave 1        D(q):   the observation scatter of the tick before (64 / TILE
+//                         lanes per env) into LDS row buffer q & 1;
+//   waves 2..     E(q-1): stream the rows of the tick before that to HBM and
+//                         clear them.
+// One workgroup barrier per tick.  C(q+1) and D(q) run at the same time, so the
+// env state is double-buffered by tick parity: grid rows and inventory rows of
+// tick q live in buffer q & 1.  C(q+1) first brings its buffer (which holds tick
+// q-1) up to tick q — a tick changes at most one cell per env (grab, bridge,
+// axe) or restarts the episode, recorded in `chg` — and copies the inventory,
+// then runs the tick on it.  Everything else (work units, hand-off, outputs,
+// statistics) is as in craft_rollout.h, and the results are identical (the same
+// tests run both kernels).
+#pragma once
+#include "craft_obs.h"
+
+namespace craft {
+
+// LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation
+// rows [2][up16(TILE*F)] | inventory rows [2][TILE][36] | agent words [2][TILE] |
+// task table [64] u16 | recipe words [16][3] | control words [4].
+__host__ __device__ inline int split_lds_bytes(int tile, int GS, int F) {
+  auto up16 = [](int x) { return (x + 15) & ~15; };
+  return up16(3 * tile * GS) + 2 * up16(tile * F) + 2 * tile * kInvStride + 2 * tile * 4 +
+         CRAFT_MAX_TASKS * 2 + CRAFT_MAX_RECIPES * 12 + 16;
+}
+
+template <int WIN, int TILE, int NT, int FMT, int WPE, bool GIVEN>
+__global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  static_assert(NT >= 192 && TILE <= 64, "a producer, a scatter wave and at least one streaming wave");
+  constexpr int P = 64 / TILE;                            // scatter lanes per env
+  auto up16 = [](int x) { return (x + 15) & ~15; };
+  const int GS = v.GS, F = v.F;
+  uint8_t* s_grid = smem;                                 // [2][TILE][GS] by tick parity
+  uint8_t* s_pristine = smem + 2 * TILE * GS;             // [TILE][GS] pool[scenario]
+  const int obs_buf = up16(TILE * F);
+  uint8_t* s_obs = smem + up16(3 * TILE * GS);            // [2][obs_buf]
+  uint8_t* s_inv = s_obs + 2 * obs_buf;                   // [2][TILE][kInvStride]
+  uint32_t* s_agent = reinterpret_cast<uint32_t*>(s_inv + 2 * TILE * kInvStride);   // [2][TILE]
+  uint16_t* s_task = reinterpret_cast<uint16_t*>(s_agent + 2 * TILE);
+  uint32_t* s_rc = reinterpret_cast<uint32_t*>(s_task + CRAFT_MAX_TASKS);
+  uint32_t* s_ctrl = s_rc + CRAFT_MAX_RECIPES * 3;
+
+  const int tid = threadIdx.x;
+  const int64_t n = v.n_envs;
+  const bool want_obs = a.obs != nullptr;
+  constexpr int esz = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
+  const int n_tiles = (int)((n + TILE - 1) / TILE);
+  const int n_chunks = (a.n_ticks + a.chunk - 1) / a.chunk;
+  const uint32_t n_units = (uint32_t)n_tiles * (uint32_t)n_chunks;
+
+  // wave 0, one lane per env (see craft_rollout.h for st / init_word / task_word / clr)
+  Agent s{};
+  uint64_t st = 0;
+  uint32_t init_word = 0, task_word = 0;
+  uint32_t clr = 0;          // cells cleared this episode (<= 3 ids, count, bit 31 = more)
+  uint32_t clr_prev = 0;     // the episode's clears before a restart (for the other buffer)
+  uint32_t chg = 0;          // what the last C did to its buffer: 0 nothing, 1 + cell cleared, kRestart
+  constexpr uint32_t kRestart = 0x80000000u;
+  bool live = false;
+  int64_t slot = 0;
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(s_pristine + tid * GS);
+  const uint8_t* pr = s_pristine + tid * GS;
+  auto grid_of = [&](int q) { return s_grid + (q & 1) * TILE * GS + tid * GS; };
+  auto inv_of = [&](int q) { return s_inv + (q & 1) * TILE * kInvStride + tid * kInvStride; };
+  uint32_t n_succ = 0, n_end = 0, n_step = 0;
+
+  // restore the cells of `cl` (or the whole row) of grid row g from the pristine row
+  auto restore = [&](uint8_t* g, uint32_t cl) {
+    if (cl >> 31) {
+      uint32_t* gw = reinterpret_cast<uint32_t*>(g);
+      for (int q0 = 0; q0 < (v.CS >> 2); q0 += 12) {
+        uint32_t w[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) w[j] = q0 + j < (v.CS >> 2) ? pw[q0 + j] : 0u;
+#pragma unroll
+        for (int j = 0; j < 12; ++j)
+          if (q0 + j < (v.CS >> 2)) gw[q0 + j] = w[j];
+      }
+    } else {
+      const int nc = (cl >> 24) & 3;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i < nc) {
+          const int c = (cl >> (8 * i)) & 0xff;
+          g[c] = pr[c];
+        }
+    }
+  };
+
+  // ---- C(q), local tick q = k - k0: tick k on buffer q & 1 (trainers/imitation.py:59-73) -------
+  auto tick_c = [&](int k, int q) {
+    const int64_t tick = a.tick0 + k;
+    const int64_t r = tick % a.ring;
+    int d = 0, succ = -1, counted = 0;
+    uint8_t* g = grid_of(q);
+    uint8_t* iv = inv_of(q);
+    s = unpack_state(st);
+    if (live) {
+      // bring this buffer (tick q-2) up to tick q-1: the other buffer's last change, inventory copy
+      if (q > 0) {
+        if (chg == kRestart) restore(g, clr_prev);
+        else if (chg) g[chg - 1] = 0;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(inv_of(q - 1));
+        uint32_t w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = src[i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(iv)[i] = w[i];
+      }
+      chg = 0;
+      int act;
+      if (GIVEN) {
+        act = a.actions[(int64_t)k * n + slot];
+      } else {
+        const uint64_t gid = (uint64_t)(v.env_base + slot);
+        act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)tick) >> 32) % 6u);
+      }
+      bool restart = false;
+      if (s.frozen) {
+        d = 1;
+      } else {
+        counted = 1;
+        s.timer -= 1;
+        d = (act == CRAFT_STOP) || s.timer <= 0;
+        restart = d && (a.flags & CRAFT_STEP_AUTORESET);
+      }
+      if (d) {                                          // satisfies() of the pre-step state
+        const int goal = task_word & 0xf, arg = (task_word >> 4) & 0xff;
+        const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));
+        if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) succ = iv[arg] > 0;
+        else if (goal == CRAFT_GOAL_GO) succ = (int)g[fc] == arg;
+        else succ = -1;
+      }
+      if (restart) {                                    // CraftScenario.init, craft.py:268-273
+        s.x = init_word & 0xff; s.y = (init_word >> 8) & 0xff; s.dir = (init_word >> 16) & 3;
+        s.timer = v.maxT;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) reinterpret_cast<uint32_t*>(iv)[w] = 0u;
+        restore(g, clr);
+        clr_prev = clr;
+        clr = 0;
+        chg = kRestart;
+      } else if (d && !s.frozen) {
+        s.frozen = 1;
+        s.timer = max(s.timer, 0);
+      }
+      if (!d) {
+        bool inv_changed = false, mask_changed = false;
+        uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
+#ifndef CRAFT_ABL_NOTRANS
+        if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
+        else transition(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed);
+#endif
+        if (mask_changed) {
+          chg = 1u + (uint32_t)fc;
+          const uint32_t nc = (clr >> 24) & 3;
+          clr = (clr >> 31) ? clr
+              : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)fc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
+        }
+      }
+      st = pack_state(s);
+      const int64_t o = r * n + slot;
+      if (a.done) a.done[o] = (uint8_t)d;
+      if (a.sat) a.sat[o] = (int8_t)succ;
+      if (a.reward) a.reward[o] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+    }
+    const uint64_t bs = __ballot(live && counted && d && succ == 1);
+    const uint64_t be = __ballot(live && counted && d);
+    const uint64_t bt = __ballot(live && counted);
+    n_succ += (uint32_t)__popcll(bs);
+    n_end += (uint32_t)__popcll(be);
+    n_step += (uint32_t)__popcll(bt);
+    s_agent[(q & 1) * TILE + tid] =
+        live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
+  };
+
+  // ---- D(q) on wave 1: lane l scatters part l / TILE of env l % TILE --------------------------
+  auto scatter_d = [&](int q, int nE) {
+    const int l = tid - 64, e = l % TILE;
+    const uint32_t ag = s_agent[(q & 1) * TILE + e];
+#ifdef CRAFT_ABL_NOD
+    if (false)
+#else
+    if (e < nE && ag)
+#endif
+      scatter_env_part<WIN, P>(v, s_grid + (q & 1) * TILE * GS + e * GS,
+                               s_inv + (q & 1) * TILE * kInvStride + e * kInvStride, ag,
+                               s_obs + (q & 1) * obs_buf + e * F, l / TILE);
+  };
+
+  // ---- once per workgroup: task table, cleared observation rows --------------------------------
+  for (int t = tid; t < v.n_tasks; t += NT) s_task[t] = v.task_tab[t];
+  for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += NT) s_rc[t] = v.rcw[t];
+  if (want_obs) {
+    uint4* z = reinterpret_cast<uint4*>(s_obs);
+    for (int i = tid; i < (2 * obs_buf >> 4); i += NT) z[i] = make_uint4(0, 0, 0, 0);
+  }
+
+  for (;;) {
+    if (tid == 0) s_ctrl[0] = (uint32_t)atomicAdd(a.queue, 1ull);
+    __syncthreads();                                    // also: s_task / rows ready
+    const uint32_t u = s_ctrl[0];
+    if (u >= n_units) break;                            // workgroup-uniform exit
+    const int t = (int)(u % (uint32_t)n_tiles), c = (int)(u / (uint32_t)n_tiles);
+    const int k0 = c * a.chunk, k1 = min(a.n_ticks, k0 + a.chunk);
+    const int nq = k1 - k0;
+    const int64_t env0 = (int64_t)t * TILE;
+    const int nE = (int)min((int64_t)TILE, n - env0);
+
+    // ---- A: wave 0 takes over the tile (after its previous chunk is published) ----------------
+    if (tid < 64) {
+      if (c > 0) {
+        bool ok = true;
+        if (tid == 0) {
+          const gu32* f = (const gu32*)(a.tile_done + t);
+          for (uint32_t spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)c;) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 26)) { ok = false; break; }   // bounded: never hang the GPU
+          }
+          if (!ok) latch_error(v.err, CRAFT_EINVARIANT, env0);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      if (tid < TILE) {
+        slot = env0 + tid;
+        live = tid < nE;
+        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        uint32_t ivr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (live) {
+          st = v.state[slot];
+          init_word = v.init[slot];
+          const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
+          const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+          ivr[0] = i0.x; ivr[1] = i0.y; ivr[2] = i0.z; ivr[3] = i0.w;
+          ivr[4] = i1.x; ivr[5] = i1.y; ivr[6] = i1.z; ivr[7] = i1.w;
+          m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
+          m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
+          s = unpack_state(st);
+          if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
+            latch_error(v.err, CRAFT_EINVAL, slot);
+            live = false;
+          }
+        }
+        chg = 0;
+        clr = 0;
+        clr_prev = 0;
+        if (live) {
+          task_word = s_task[s.task];
+          // pool[scenario] -> the pristine row and both grid buffers; inventory -> both buffers
+          uint32_t* g0 = reinterpret_cast<uint32_t*>(s_grid + tid * GS);
+          uint32_t* g1 = reinterpret_cast<uint32_t*>(s_grid + TILE * GS + tid * GS);
+          uint32_t* pwm = reinterpret_cast<uint32_t*>(s_pristine + tid * GS);
+          const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
+          const int nchunk = v.CS >> 4;
+          for (int q0 = 0; q0 < nchunk; q0 += 4) {
+            uint4 cq[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (q0 + j < nchunk) cq[j] = src[q0 + j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (q0 + j < nchunk) {
+                const int q = 4 * (q0 + j);
+                pwm[q + 0] = g0[q + 0] = g1[q + 0] = cq[j].x;
+                pwm[q + 1] = g0[q + 1] = g1[q + 1] = cq[j].y;
+                pwm[q + 2] = g0[q + 2] = g1[q + 2] = cq[j].z;
+                pwm[q + 3] = g0[q + 3] = g1[q + 3] = cq[j].w;
+              }
+          }
+          uint32_t* iv0 = reinterpret_cast<uint32_t*>(s_inv + tid * kInvStride);
+          uint32_t* iv1 = reinterpret_cast<uint32_t*>(s_inv + TILE * kInvStride + tid * kInvStride);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) iv0[i] = iv1[i] = ivr[i];
+          uint8_t* b0 = s_grid + tid * GS;
+          uint8_t* b1 = s_grid + TILE * GS + tid * GS;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {                 // cells cleared this episode
+            uint32_t mm = m[w];
+            while (mm) {
+              const int cc = w * 32 + __ffs(mm) - 1;
+              b0[cc] = 0;
+              b1[cc] = 0;
+              const uint32_t nc = (clr >> 24) & 3;
+              clr = (clr >> 31) ? clr
+                  : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)cc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
+              mm &= mm - 1;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        tick_c(k0, 0);                                  // C(0) -> buffer 0
+      }
+    }
+
+    // ---- the pipeline: interval i runs C(i+1) | D(i) | E(i-1), one barrier each -------------
+    if (!want_obs) {
+      if (tid < TILE)
+        for (int q = 1; q < nq; ++q) tick_c(k0 + q, q);
+    } else {
+      __syncthreads();                                  // C(0) complete
+      if (tid < 64) {
+        for (int i = 0; i <= nq; ++i) {
+          if (tid < TILE && i + 1 < nq) tick_c(k0 + i + 1, i + 1);
+          __syncthreads();
+        }
+      } else if (tid < 128) {
+        for (int i = 0; i <= nq; ++i) {
+          if (i < nq) scatter_d(i, nE);
+          __syncthreads();
+        }
+      } else {
+        const int et = tid - 128;
+        for (int i = 0; i <= nq; ++i) {
+          if (i >= 1) {
+            const int q = i - 1;
+            const int64_t r = (a.tick0 + k0 + q) % a.ring;
+            void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
+#ifndef CRAFT_ABL_NOE
+            (void)out;
+#else
+            (void)out;
+#endif
+          }
+          __syncthreads();
+        }
+      }
+    }
+
+    // ---- publish the tile for the unit (t, c + 1) (as craft_rollout.h) ---------------------------
+    const bool state_only = a.ring >= a.n_ticks;
+    const bool handoff = c + 1 < n_chunks;
+    if (tid < TILE && live) {
+      const int ql = nq - 1;                            // the buffer of the last tick
+      const uint32_t* gw = reinterpret_cast<const uint32_t*>(grid_of(ql));
+      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of(ql));
+      uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int q = 0; q < (v.CS >> 2); ++q) {
+        const uint32_t p = pw[q], cc = gw[q];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const bool cleared = ((p >> (8 * b)) & 0xffu) != 0 && ((cc >> (8 * b)) & 0xffu) == 0;
+          const int cell = 4 * q + b;
+          if (cleared) m[cell >> 5] |= 1u << (cell & 31);
+        }
+      }
+      if (handoff && state_only) {
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t inv_r = __builtin_amdgcn_make_buffer_rsrc(v.inv, 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t msk_r = __builtin_amdgcn_make_buffer_rsrc(v.mask, 0, 0x7fffffff, 0x00020000);
+        const int off = (int)(slot * 32);
+        __hip_atomic_store((gu64*)(v.state + slot), (unsigned long long)st, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[0], ivw[1], ivw[2], ivw[3]}, inv_r, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[4], ivw[5], ivw[6], ivw[7]}, inv_r, off + 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{m[0], m[1], m[2], m[3]}, msk_r, off, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u4v{m[4], m[5], m[6], m[7]}, msk_r, off + 16, 0, 16);
+      } else {
+        v.state[slot] = st;
+        v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+        v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
+        v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
+        v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
+      }
+    }
+    if (handoff && state_only) {
+      if (tid < 64) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0)
+          __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (handoff) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();                                    // s_ctrl and the LDS rows are reused
+  }
+
+  if (tid == 0) {
+    unsigned long long* srow = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
+    atomicAdd(srow + 0, (unsigned long long)n_succ);
+    atomicAdd(srow + 1, (unsigned long long)n_end);
+    atomicAdd(srow + 2, (unsigned long long)n_step);
+  }
+}
+
+}  // namespace craft
