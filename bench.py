@@ -6,10 +6,15 @@ This is BASELINE.json's metric on 12x12 craft_medium with 65536 envs per GPU
 (configs[2]); configs[3] is the 8-GPU sharding of the same.
 
 Actions are the hashed random draw (the random-rollout workload), so ticks are
-launched K = 32 at a time through craft_rollout. Every tick still does all of
-its work and writes its full observation, reward, done and success to HBM; the
-envs just stay on chip between ticks. --ticks-per-launch 1 times one craft_step
-launch per tick instead.
+launched up to K = 32 at a time through craft_rollout: `--steps S` runs S // K
+launches of K ticks plus one launch of the remainder.  Every tick still does
+all of its work and writes its full observation, reward, done and success to
+HBM; the envs just stay on chip between ticks.  --ticks-per-launch 1 times
+one craft_step launch per tick instead.
+
+--workload teacher is configs[4]: every tick also runs the on-GPU
+DemonstrationTeacher (teachers/demonstration.py) for every env, the DAgger
+label of that tick's state.
 
 Inputs (scenario pool, env states) are resident in HBM before the timed region.
 Observations stream into a ring of R = 16 device buffers (1.7 GB, 6.6x the
@@ -18,16 +23,19 @@ Observations stream into a ring of R = 16 device buffers (1.7 GB, 6.6x the
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
-Rank 0 prints one JSON line (see the contract in the task description).
+`--gpus N > 1` without torchrun's environment starts N rank processes itself
+(python -m torch.distributed.run) before touching the GPU.  Rank 0 prints one
+JSON line (see the contract in the task description).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -35,20 +43,37 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def bytes_per_env_step(W, H, window, F):
+def bytes_per_env_step(W, H, window, F, teacher=False):
     """Algorithmic HBM bytes per env-step: 57 B of step state
     (action 1 + agent state r/w 48 + facing/target cells 2 + cell write 1 +
     reward 4 + done 1) + the fp32 observation row F*4 + the pooled window's
-    grid cells min(w^2, W) * min(w^2, H)."""
+    grid cells min(w^2, W) * min(w^2, H); the teacher adds the W*H navigation
+    grid + the 2 B task id, and its 4 B label ("C5 adds the
+    teacher reads")."""
     ww = window * window
-    return 57 + 4 * F + min(ww, W) * min(ww, H)
+    b = 57 + 4 * F + min(ww, W) * min(ww, H)
+    if teacher:
+        b += W * H + 2 + 4
+    return b
 
 
-def parse():
+def plan_launches(steps, k):
+    """Launch sizes (ticks per launch) covering `steps` ticks: steps // k
+    launches of k ticks, then one of the remainder."""
+    if steps < 0 or k < 1:
+        raise ValueError("need steps >= 0 and ticks-per-launch >= 1")
+    full, rem = divmod(steps, k)
+    return [k] * full + ([rem] if rem else [])
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=1024)
     p.add_argument("--warmup", type=int, default=64)
+    p.add_argument("--workload", choices=("rollout", "teacher"), default="rollout",
+                   help="rollout: configs[2] (random rollout, full features); "
+                        "teacher: configs[4] (+ the BFS DemonstrationTeacher label every tick)")
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--world", default="craft_medium_12x12")
     p.add_argument("--pool", type=int, default=1024)
@@ -59,40 +84,101 @@ def parse():
                    help="0 write-back, 1 nontemporal, 2 sc1; -1: the measured best for the path "
                         "(nontemporal for craft_step, write-back for craft_rollout)")
     p.add_argument("--ticks-per-launch", type=int, default=32,
-                   help="K > 1: craft_rollout runs K ticks per launch (the same work per tick); "
-                        "1: one craft_step launch per tick")
+                   help="K > 1: craft_rollout runs up to K ticks per launch (the same work per "
+                        "tick); 1: one craft_step launch per tick")
     p.add_argument("--rollout-threads", type=int, default=0,
-                   help="craft_rollout threads per tile workgroup (0 = 8 per env: 7 streaming waves)")
+                   help="craft_rollout threads per tile workgroup (0 = the library's default shape)")
     p.add_argument("--rollout-chunk", type=int, default=0,
                    help="craft_rollout ticks per dynamically scheduled work unit (0 = the whole launch)")
     p.add_argument("--obs-only", action="store_true",
                    help="diagnostic: skip the reward/done/success rings (not a bench line)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-seconds", type=float, default=8.0,
+                   help="wall seconds of each cpu_baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    return p.parse_args()
+    p.add_argument("--traffic", default=None,
+                   help="PMC traffic JSON (tools/pmc_summary.py); default profiles/pmc_traffic*.json")
+    args = p.parse_args(argv)
+    # everything is validated here, before any process is started or any GPU call is made
+    if args.gpus < 1:
+        p.error("--gpus must be >= 1")
+    if args.steps < 1 or args.warmup < 0:
+        p.error("--steps must be >= 1 and --warmup >= 0")
+    if args.ticks_per_launch < 1:
+        p.error("--ticks-per-launch must be >= 1")
+    if args.envs < 1 or args.pool < 1 or args.ring < 1:
+        p.error("--envs, --pool and --ring must be >= 1")
+    if args.tile not in (0, 16, 32, 64):
+        p.error("--tile must be 0, 16, 32 or 64")
+    if args.workload == "teacher" and args.ticks_per_launch != 1:
+        # the teacher labels each tick's state, so ticks are launched one at a time
+        args.ticks_per_launch = 1
+    return args
 
 
-def cpu_baseline(sim, grids, specs, seconds):
-    """The CPU oracle (C restatement) on a bounded sample of the same workload,
-    one thread per host core given to this job (OMP_NUM_THREADS; 16 on the GPU
-    box), each on its own slice of envs; env-steps/s.  ctypes releases the GIL
-    around every oracle call, so the threads run in parallel."""
+def world_check(args, env=None):
+    """What to do about the process topology: "spawn" (no torchrun environment
+    and --gpus > 1: start the ranks), "run", or an error message when
+    WORLD_SIZE disagrees with --gpus."""
+    env = os.environ if env is None else env
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if args.gpus > 1 else "run"
+    if int(ws) != args.gpus:
+        return f"WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to report a different node size"
+    return "run"
+
+
+def spawn_ranks(args, argv):
+    """Start one rank per GPU with torch.distributed.run as a CHILD process (this
+    process has not touched the GPU) and return its exit code."""
+    import torch
+    have = torch.cuda.device_count()          # counts devices without initialising HIP
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---- CPU baseline ----------------------------------------------------------------------------
+def _cores():
+    n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def cpu_baseline_c(cfg, grids, specs, env_id_base, seed, seconds):
+    """The C restatement (oracle/craft_oracle.c oracle_bench) on a bounded sample
+    of the same workload, one thread per host core given to this job, each on
+    its own contiguous slice of global env ids, every env writing its own
+    observation row; env-steps/s.  ctypes releases the GIL around each call."""
     import threading
     import oracle
+    oracle.build()
     n = 4096
-    cores = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
-    o = oracle.Oracle(sim.config, grids)
+    cores = _cores()
+    o = oracle.Oracle(cfg, grids)
     envs = o.init_envs(*[a[:n] for a in specs])
-    parts = [envs[i::cores].copy() for i in range(cores)]
+    bounds = np.linspace(0, n, cores + 1).astype(int)
+    parts = [(envs[bounds[i]:bounds[i + 1]].copy(), env_id_base + int(bounds[i])) for i in range(cores)]
+    bufs = [o.bench_buffers(len(p[0])) for p in parts]
     steps = [0] * cores
+    ticks = [0] * cores
     t0 = time.perf_counter()
     deadline = t0 + seconds
 
     def work(i):
+        e, base = parts[i]
         while time.perf_counter() < deadline:
-            steps[i] += o.bench(parts[i], 20, seed=1)
+            steps[i] += o.bench(e, base, ticks[i], 4, seed, bufs[i])
+            ticks[i] += 4
 
     threads = [threading.Thread(target=work, args=(i,)) for i in range(cores)]
     for t in threads:
@@ -102,14 +188,28 @@ def cpu_baseline(sim, grids, specs, seconds):
     dt = time.perf_counter() - t0
     total = sum(steps)
     return {"value": total / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
-            "sample": f"{n} envs x {total // n} ticks ({dt:.1f} s) of the same workload "
-                      "(12x12 craft_medium, hashed actions, auto-reset): step + satisfies + "
-                      f"full features() per env-step, oracle/craft_oracle.c, {cores} threads "
-                      "on disjoint env slices"}
+            "sample": f"{n} envs x {total // n} ticks ({dt:.1f} s) of the same workload (12x12 "
+                      "craft_medium, global-id hashed actions, auto-reset): step + satisfies + full "
+                      "features() with obs/reward/done/success written to each env's own row; "
+                      f"oracle/craft_oracle.c (gcc -O3), {cores} threads on contiguous env slices"}
 
 
-def main():
-    args = parse()
+def cpu_baseline_numpy(cfg, grids, specs, env_id_base, seed, seconds):
+    """The pure-Python/numpy restatement (oracle/craft_numpy.py: the reference's
+    per-env loop and data layout) over all the job's cores as processes."""
+    from oracle import craft_numpy
+    n = 1024
+    rate, procs, total, dt = craft_numpy.bench(cfg, grids, np.stack(specs, 1)[:n], env_id_base,
+                                               seed, seconds)
+    return {"value": rate, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{n} envs, {total} env-steps in {dt:.1f} s: oracle/craft_numpy.py "
+                      "(float64 one-hot grids, per-env step/features/satisfies as in "
+                      f"worlds/craft.py), {procs} processes on contiguous env slices"}
+
+
+# ---- the GPU run -----------------------------------------------------------------------------
+def run(args):
+    import torch
     from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
     from psketch_amd import distributed as D
 
@@ -118,12 +218,17 @@ def main():
     dev = torch.device("cuda", local_rank)
     D.init(device=dev)                        # RCCL process group when WORLD_SIZE > 1
 
+    teacher = args.workload == "teacher"
+    K = 1 if teacher else args.ticks_per_launch
+    timed_plan = plan_launches(args.steps, K)
+    warm_plan = plan_launches(args.warmup, K)
+    k_eff = timed_plan[0]                     # = min(K, steps): the launch the events time
+
     env_base, n = D.env_shard(rank, args.envs)
     sim = CraftSim(args.world, n_envs=n, device=local_rank, env_id_base=env_base,
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
-    K = max(1, args.ticks_per_launch)
     obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 0)
     sim.tune(args.tile, 0, obs_store)
     sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
@@ -133,84 +238,101 @@ def main():
     sim.reset(*specs)
     F = sim.n_features
     R = args.ring
-    if args.steps % K or args.warmup % K:
-        raise SystemExit("--steps and --warmup must be multiples of --ticks-per-launch")
     ring = torch.empty((R, n, F), dtype=sim.obs_dtype, device=dev)     # one tick's obs per slot
     reward = torch.empty((R, n), dtype=torch.float32, device=dev)
     done = torch.empty((R, n), dtype=torch.uint8, device=dev)
     success = torch.empty((R, n), dtype=torch.int8, device=dev)
+    labels = torch.empty((R, n), dtype=torch.int32, device=dev)
 
     tick = 0
 
-    def launch():
-        """K ticks: one craft_step (K = 1) or one craft_rollout launch."""
+    def launch(k):
+        """k ticks: one craft_rollout launch, or k craft_step (+ teacher) launches."""
         nonlocal tick
         if K == 1:
-            r = tick % R
-            sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r], done=done[r],
-                     success=success[r])
+            for _ in range(k):
+                r = tick % R
+                if teacher:
+                    sim.teacher(action_out=labels[r])      # DAgger label of the tick's state
+                sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r], done=done[r],
+                         success=success[r])
+                tick += 1
         else:
             if args.obs_only:
-                sim.rollout(K, seed=args.seed, tick0=tick, obs=ring)
+                sim.rollout(k, seed=args.seed, tick0=tick, obs=ring)
             else:
-                sim.rollout(K, seed=args.seed, tick0=tick, obs=ring, reward=reward, done=done,
+                sim.rollout(k, seed=args.seed, tick0=tick, obs=ring, reward=reward, done=done,
                             success=success)
-        tick += K
+            tick += k
 
-    for _ in range(args.warmup // K):
-        launch()
+    for k in warm_plan:
+        launch(k)
     sim.check()
 
     def barrier():
         D.barrier()
         torch.cuda.synchronize()
 
-    # ---- timed region: K ticks, barrier + synchronize on both sides ------------------
+    # ---- timed region: exactly args.steps ticks, barrier + synchronize on both sides -------
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps // K):
-        launch()
+    for k in timed_plan:
+        launch(k)
     barrier()
     elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
 
-    # ---- per-launch kernel duration, HIP events on the launch stream --------------------
+    # ---- per-launch kernel duration, HIP events on the launch stream (outside the timed
+    # region): launches of k_eff ticks, as many as the timed region had (at least 8) ----------
     kstream = torch.cuda.current_stream(dev)
-    m = max(1, min(args.steps // K, 400))
+    m = min(max(len(timed_plan), 8), 200)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(m)]
     torch.cuda.synchronize()
     for a, b in evs:
         a.record(kstream)
-        launch()
+        launch(k_eff)
         b.record(kstream)
     torch.cuda.synchronize()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))     # per launch (K ticks)
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))     # per launch (k_eff ticks)
 
-    # ---- scalar episode summary: one RCCL all-reduce of int64[3] --------------------------
+    # ---- scalar episode summary: one RCCL all-reduce of int64[3] ----------------------------
     stats = D.reduce_episode_stats(sim.stats()).cpu().tolist()
     sim.check()
 
     if rank == 0:
+        win = sim.params["WINDOW_WIDTH"]
         total_steps = n * world_size * args.steps
         value = total_steps / elapsed
-        bps = bytes_per_env_step(sim.width, sim.height, sim.params["WINDOW_WIDTH"], F)
-        win = sim.params["WINDOW_WIDTH"]
-        if K > 1 and not args.rollout_threads and win == 3:
-            tile, threads = 32, 512                      # craft_rollout's default shape (split producer)
+        bps = bytes_per_env_step(sim.width, sim.height, win, F, teacher)
+        if K > 1:
+            tile, threads, split = sim.rollout_shape()          # what the library launched
+            fmt = {"f32": "0", "bf16": "1", "u8": "2"}[sim.obs_format]
+            kname = (f"rollout_split_kernel<{win}, {tile}, {threads}, {fmt}, *, false>" if split
+                     else f"rollout_kernel<{win}, {tile}, {threads}, {fmt}, *, false>")
+            shape = {"tile": tile, "rollout_threads": threads, "split_producer": split,
+                     "rollout_chunk": args.rollout_chunk or k_eff}
         else:
-            tile = args.tile or {3: 64, 5: 32}.get(win, 16)
-            threads = args.rollout_threads or 8 * tile
-        achieved = bps * n * K / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        workload = f"{args.world}_w{sim.params['WINDOW_WIDTH']}_B{n}_random_rollout_full_features"
+            tile, _ = sim.tile_shape()
+            kname = f"tile_kernel<{win}, MODE_TICK, {tile}>"
+            if teacher:
+                kname += " + teacher_kernel"
+            shape = {"tile": tile}
+        achieved = bps * n * k_eff / (kernel_ms * 1e-3) / 1e9
+        workload = f"{args.world}_w{win}_B{n}_" + (
+            "teacher_labels_full_features" if teacher else "random_rollout_full_features")
         if K > 1:
             workload += f"_K{K}"
-        if os.path.exists(args.traffic):
+        traffic = None
+        tpath = args.traffic or os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath):
             try:
-                tj = json.load(open(args.traffic))
-                if tj.get("workload") == workload:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
+                with open(tpath) as f:
+                    tj = json.load(f)
+                entries = tj if isinstance(tj, list) else [tj]
+                for e in entries:
+                    if e.get("workload") == workload and e.get("ticks_per_launch", K) == k_eff:
+                        traffic = e.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
                 traffic = None
         line = {
             "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
@@ -223,32 +345,49 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": "fp32",
             "data": "synthetic: 1024 make_data.sample_scenario worlds (RandomState(123)), "
                     "per-env init keyed by global id, splitmix64 actions",
-            "config": {"workload": workload, "world": args.world, "envs_per_gpu": n,
-                       "global_batch": n * world_size, "window": sim.params["WINDOW_WIDTH"],
-                       "n_features": F, "obs_dtype": "fp32", "obs_ring": args.ring,
-                       "pool": args.pool, "parallelism": f"env-shard x{world_size}",
-                       "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
-                       "tile": tile, "rollout_threads": threads,
-                       "rollout_chunk": args.rollout_chunk or K, "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]},
+            "config": dict({"workload": workload, "world": args.world, "envs_per_gpu": n,
+                            "global_batch": n * world_size, "window": win,
+                            "n_features": F, "obs_dtype": "fp32",
+                            "state_dtype": "u8 (exact small integers; the reference's float64 "
+                                           "arrays hold the same values)",
+                            "obs_ring": args.ring, "pool": args.pool,
+                            "parallelism": f"env-shard x{world_size}",
+                            "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
+                            "launches": len(timed_plan),
+                            "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]}, **shape),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": (f"tile_kernel<{sim.params['WINDOW_WIDTH']}, MODE_TICK, {tile}>"
-                                    if K == 1 else
-                                    (f"rollout_split_kernel<{win}, {tile}, {threads}>"
-                                     if tile <= 32 and threads >= 320
-                                     else f"rollout_kernel<{win}, {tile}, {threads}>")),
-                         "kernel_us": kernel_ms * 1e3, "ticks_per_launch": K,
-                         "bytes_per_launch": bps * n * K, "bytes_per_env_step": bps},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
+                         "kernel_us": kernel_ms * 1e3, "ticks_per_launch": k_eff,
+                         "bytes_per_launch": bps * n * k_eff, "bytes_per_env_step": bps},
             "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},
         }
         if world_size == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(sim, grids, specs, args.cpu_seconds)
+            c_leg = cpu_baseline_c(sim.config, grids, specs, env_base, args.seed, args.cpu_seconds)
+            try:
+                np_leg = cpu_baseline_numpy(sim.config, grids, specs, env_base, args.seed,
+                                            args.cpu_seconds)
+            except Exception as e:          # the C leg stands alone if process pools are refused
+                np_leg = {"error": f"{type(e).__name__}: {e}"}
+            line["cpu_baseline"] = dict(c_leg, python_numpy=np_leg)
         print(json.dumps(line), flush=True)
     D.shutdown()
 
 
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    what = world_check(args)
+    if what == "spawn":
+        return spawn_ranks(args, argv)
+    if what != "run":
+        print(f"bench.py: {what}", file=sys.stderr)
+        return 2
+    run(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

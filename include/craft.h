@@ -159,8 +159,19 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * tiles also take 512.  16- and 32-env tiles with 320, 384 or 512: the
  * split-producer kernel (transition and scatter on two waves, the other 3-6
  * stream).  0 (default) = the measured best: 32-env tiles x 512 threads (split)
- * for 3x3 windows, else the handle's tile with 8 threads per env. */
+ * for 3x3 windows, else the handle's tile with 256 threads (512 for 64-env tiles). */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
+
+/* The launch shape the next craft_rollout will use, resolved from the knobs above:
+ * envs per tile workgroup, threads per workgroup, and split = 1 for the
+ * split-producer kernel (rollout_split_kernel), 0 for rollout_kernel.  Lets a
+ * caller (bench.py) name the kernel it times instead of mirroring the defaults. */
+int craft_sim_rollout_shape(const craft_sim_t* sim, int32_t* tile_envs, int32_t* threads,
+                            int32_t* split);
+
+/* The tile kernel's current envs per workgroup and observation store policy
+ * (craft_sim_tune), for the same purpose on the craft_step path. */
+int craft_sim_tile_shape(const craft_sim_t* sim, int32_t* tile_envs, int32_t* obs_store);
 
 /* Element type of every observation buffer this handle writes (craft_reset,
  * craft_step, craft_step_ex, craft_observe).  The features are small

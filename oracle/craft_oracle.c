@@ -283,23 +283,17 @@ int oracle_batch_tick(const craft_config_t* cfg, const uint8_t* pool, oracle_env
 }
 
 int64_t oracle_bench(const craft_config_t* cfg, const uint8_t* pool, oracle_env_t* envs,
-                     int64_t n, int64_t ticks, uint64_t seed, float* scratch_row) {
-  int64_t steps = 0;
+                     int64_t n, int64_t env_id_base, int64_t tick0, int64_t ticks, uint64_t seed,
+                     float* obs, float* reward, uint8_t* done, int8_t* success, int64_t* stats) {
+  /* The GPU bench's work, tick for tick: the do_rollout protocol with hashed
+   * actions keyed by global id, auto-reset, and every output written to its own
+   * row (obs [n][F], reward/done/success [n]) — the same stores the GPU is
+   * charged for. */
   for (int64_t t = 0; t < ticks; ++t)
-    for (int64_t e = 0; e < n; ++e) {
-      oracle_env_t* s = &envs[e];
-      int32_t a = oracle_hash_action(seed, e, t);
-      s->timer -= 1;
-      if (a == CRAFT_STOP || s->timer <= 0) {
-        (void)oracle_satisfies(cfg, s, s->task);
-        oracle_reset(cfg, pool, s);
-      } else {
-        oracle_step(cfg, s, a);
-      }
-      oracle_features(cfg, s, scratch_row);
-      ++steps;
-    }
-  return steps;
+    if (oracle_batch_tick(cfg, pool, envs, n, env_id_base, NULL, seed, tick0 + t,
+                          CRAFT_STEP_AUTORESET, obs, reward, done, success, stats))
+      return -1;
+  return n * ticks;
 }
 
 int oracle_sizeof_config(void) { return (int)sizeof(craft_config_t); }

@@ -112,6 +112,9 @@ SIGNATURES = {
     "craft_sim_tune": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),
+    "craft_sim_rollout_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
+                                       ctypes.POINTER(_i32)]),
+    "craft_sim_tile_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "craft_pool_load": (_i32, [_vp, _vp, _i32, _i32]),
     "craft_pool_generate": (_i32, [_vp, _u64, _i64, _i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32,
                                    _vp, _vp]),

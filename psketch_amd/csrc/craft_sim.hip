@@ -222,6 +222,22 @@ size_t lds_bytes(const craft_sim* s, int tile, int obs_bufs = 1, bool pristine =
   return b;
 }
 
+// The workgroup shape craft_rollout launches with (craft_sim_rollout_shape).  Default
+// (threads 0): for 3x3 windows the split-producer kernel on 32-env tiles with 6
+// streaming waves (7-15 % faster than 64-env tiles at 65536 envs);
+// otherwise the handle's tile with 256 threads (512 for 64-env tiles).
+void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
+  int t = s->tile, nt = s->rollout_threads;
+  if (nt == 0 && s->cfg.window_width == 3) {
+    t = 32;
+    nt = 512;
+  }
+  if (nt == 0) nt = (t == 64) ? 512 : 256;   // launch_rollout_win's defaults
+  *tile = t;
+  *threads = nt;
+  *split = (t <= 32 && nt >= 320) ? 1 : 0;
+}
+
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
   hipError_t e = craft::launch_tile(mode, s->cfg.window_width, s->tile, s->view, a, lds_bytes(s, s->tile),
                                     reinterpret_cast<hipStream_t>(stream));
@@ -418,6 +434,23 @@ int craft_sim_info(const craft_sim_t* s, int64_t* n_envs, int32_t* pool_capacity
   return CRAFT_OK;
 }
 
+int craft_sim_rollout_shape(const craft_sim_t* s, int32_t* tile_envs, int32_t* threads, int32_t* split) {
+  if (!s) return CRAFT_EINVAL;
+  int t = 0, nt = 0, sp = 0;
+  rollout_shape(s, &t, &nt, &sp);
+  if (tile_envs) *tile_envs = t;
+  if (threads) *threads = nt;
+  if (split) *split = sp;
+  return CRAFT_OK;
+}
+
+int craft_sim_tile_shape(const craft_sim_t* s, int32_t* tile_envs, int32_t* obs_store) {
+  if (!s) return CRAFT_EINVAL;
+  if (tile_envs) *tile_envs = s->tile;
+  if (obs_store) *obs_store = s->view.obs_policy;
+  return CRAFT_OK;
+}
+
 int craft_sim_check(craft_sim_t* s, int64_t* env_out, void* stream) {
   if (!s) return CRAFT_EINVAL;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -573,14 +606,8 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   a.tile_done = reinterpret_cast<uint32_t*>(s->d_sync + 16);
   if (n_ticks > 0)
     HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
-  // default shape (threads 0): for 3x3 windows the split-producer kernel on 32-env tiles
-  // with 6 streaming waves (7-15 % faster than 64-env tiles at 65536 envs);
-  // otherwise the handle's tile
-  int tile = s->tile, threads = s->rollout_threads;
-  if (threads == 0 && s->cfg.window_width == 3) {
-    tile = 32;
-    threads = 512;
-  }
+  int tile = 0, threads = 0, split = 0;
+  rollout_shape(s, &tile, &threads, &split);
   hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, s->view, a, lds_bytes(s, tile, 2, true),
                                        reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");

@@ -87,6 +87,21 @@ class CraftSim:
         self._check(N.lib().craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
                     "craft_sim_tune_rollout")
 
+    def rollout_shape(self):
+        """(tile_envs, threads, split) the next rollout() launches with, as the
+        library resolves its knobs (craft_sim_rollout_shape)."""
+        t, nt, sp = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._check(N.lib().craft_sim_rollout_shape(self._h, ctypes.byref(t), ctypes.byref(nt),
+                                                    ctypes.byref(sp)), "craft_sim_rollout_shape")
+        return t.value, nt.value, bool(sp.value)
+
+    def tile_shape(self):
+        """(tile_envs, obs_store) of the tick kernel (craft_sim_tile_shape)."""
+        t, st = ctypes.c_int32(), ctypes.c_int32()
+        self._check(N.lib().craft_sim_tile_shape(self._h, ctypes.byref(t), ctypes.byref(st)),
+                    "craft_sim_tile_shape")
+        return t.value, st.value
+
     _OBS_FORMATS = {"f32": (N.OBS_F32, torch.float32), "bf16": (N.OBS_BF16, torch.bfloat16),
                     "u8": (N.OBS_U8, torch.uint8)}
 
@@ -122,14 +137,32 @@ class CraftSim:
             raise ValueError(f"expected {n} entries, got {t.numel()}")
         return t
 
+    def _buf(self, name, t, dtype, shape):
+        """Checks a caller-owned output (or input) tensor before its pointer goes
+        to the C ABI: dtype, contiguity, exact shape and device.  A wrong buffer
+        raises here instead of letting a kernel write out of bounds."""
+        if t is None:
+            return None
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a torch tensor")
+        if t.dtype != dtype:
+            raise TypeError(f"{name} is {t.dtype}, expected {dtype}")
+        if t.device != self.device:
+            raise ValueError(f"{name} is on {t.device}, the simulator is on {self.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {tuple(shape)}")
+        return t
+
     def empty_obs(self, n=None):
         n = self.n_envs if n is None else n
         return torch.empty((n, self.n_features), dtype=self.obs_dtype, device=self.device)
 
-    def _obs(self, obs):
-        if obs is not None and obs.dtype != self.obs_dtype:
-            raise TypeError(f"obs is {obs.dtype}, the simulator writes {self.obs_dtype}")
-        return _ptr(obs)
+    def _obs(self, obs, n=None):
+        """An [n, F] observation buffer in the handle's format (n = n_envs)."""
+        n = self.n_envs if n is None else n
+        return _ptr(self._buf("obs", obs, self.obs_dtype, (n, self.n_features)))
 
     # ---- scenario pool -----------------------------------------------------------------
     def load_pool(self, grids, first=0):
@@ -189,9 +222,12 @@ class CraftSim:
                 and any_live is None and transition_code is None:
             # plain tick: the short craft_step entry (least host overhead per launch)
             a = self._i32(actions, n) if actions is not None else None
+            r = self._buf("reward", reward, torch.float32, (n,))
+            d = self._buf("done", done, torch.uint8, (n,))
+            sc = self._buf("success", success, torch.int8, (n,))
             self._check(N.lib().craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
-                                           int(tick), flags, self._obs(obs), _ptr(reward),
-                                           _ptr(done), _ptr(success), self._stream()), "craft_step")
+                                           int(tick), flags, self._obs(obs), _ptr(r),
+                                           _ptr(d), _ptr(sc), self._stream()), "craft_step")
             return obs
         args = N.craft_step_args_t()
         keep = []
@@ -209,13 +245,13 @@ class CraftSim:
             if bc.numel() != n:
                 raise ValueError(f"behavior_clone: expected {n} entries")
             put("behavior_clone", bc)
-        for name, t, dt in (("reward", reward, torch.float32), ("done", done, torch.uint8),
-                            ("success", success, torch.int8), ("action_record", action_record, torch.int32),
-                            ("any_live", any_live, torch.int32),
-                            ("transition_code", transition_code, torch.int8)):
-            if t is not None and (t.dtype != dt or not t.is_contiguous()):
-                raise TypeError(f"{name} must be a contiguous {dt} tensor")
-            put(name, t)
+        for name, t, dt, shape in (("reward", reward, torch.float32, (n,)),
+                                   ("done", done, torch.uint8, (n,)),
+                                   ("success", success, torch.int8, (n,)),
+                                   ("action_record", action_record, torch.int32, (n,)),
+                                   ("any_live", any_live, torch.int32, (1,)),
+                                   ("transition_code", transition_code, torch.int8, (n,))):
+            put(name, self._buf(name, t, dt, shape))
         self._obs(obs)
         put("obs", obs)
         args.action_seed = seed & (2**64 - 1)
@@ -231,24 +267,27 @@ class CraftSim:
         [n_ticks, N] or None (hashed); obs: [R, N, F] ring in the obs format
         (tick t writes obs[t % R]); reward / done / success: [R, N] rings."""
         n = self.n_envs
-        if obs is not None and (obs.dim() != 3 or obs.shape[1:] != (n, self.n_features)):
-            raise ValueError(f"obs must be [ring, {n}, {self.n_features}]")
-        ring = obs.shape[0] if obs is not None else None
+        if n_ticks < 0:
+            raise ValueError("n_ticks must be >= 0")
+        ring = None
+        for name, t in (("obs", obs), ("reward", reward), ("done", done), ("success", success)):
+            if t is not None:
+                if t.dim() < 1 or t.shape[0] < 1:
+                    raise ValueError(f"{name} must be a ring [R >= 1, {n}, ...]")
+                if ring is not None and t.shape[0] != ring:
+                    raise ValueError(f"{name} ring {t.shape[0]} != ring {ring} of the other outputs")
+                ring = t.shape[0]
+        if obs is not None:
+            self._buf("obs", obs, self.obs_dtype, (ring, n, self.n_features))
         for name, t, dt in (("reward", reward, torch.float32), ("done", done, torch.uint8),
                             ("success", success, torch.int8)):
-            if t is None:
-                continue
-            if t.dtype != dt or not t.is_contiguous() or t.dim() != 2 or t.shape[1] != n:
-                raise TypeError(f"{name} must be a contiguous {dt} tensor [ring, {n}]")
-            if ring is not None and t.shape[0] != ring:
-                raise ValueError(f"{name} ring {t.shape[0]} != obs ring {ring}")
-            ring = t.shape[0]
+            self._buf(name, t, dt, (ring, n) if t is not None else ())
         a = None
         if actions is not None:
             a = self._i32(actions, n * n_ticks)
         self._check(N.lib().craft_rollout(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
                                           int(tick0), int(n_ticks),
-                                          N.STEP_AUTORESET if autoreset else 0, self._obs(obs),
+                                          N.STEP_AUTORESET if autoreset else 0, _ptr(obs),
                                           int(ring or 1), _ptr(reward), _ptr(done), _ptr(success),
                                           self._stream()), "craft_rollout")
         return obs
@@ -268,8 +307,7 @@ class CraftSim:
         a = self._i32(actions)
         n = a.numel()
         s, d = self._i32(src, n), self._i32(dst, n)
-        if codes is not None and (codes.dtype != torch.int8 or codes.numel() != n):
-            raise TypeError(f"codes must be an int8 tensor of {n} entries")
+        self._buf("codes", codes, torch.int8, (n,))
         self._check(N.lib().craft_transition(self._h, _ptr(s), _ptr(d), _ptr(a), n, _ptr(codes),
                                              self._stream()), "craft_transition")
         return codes
@@ -278,7 +316,8 @@ class CraftSim:
         s = self._i32(slots)
         n = s.numel() if s is not None else (self.n_envs if n is None else n)
         t = self._i32(tasks, n)
-        self._check(N.lib().craft_observe(self._h, _ptr(s), n, _ptr(t), self._obs(obs), _ptr(sat),
+        self._buf("sat", sat, torch.int8, (n,))
+        self._check(N.lib().craft_observe(self._h, _ptr(s), n, _ptr(t), self._obs(obs, n), _ptr(sat),
                                           self._stream()), "craft_observe")
         return obs, sat
 
@@ -288,6 +327,8 @@ class CraftSim:
         t = self._i32(tasks, n)
         if action_out is None:
             action_out = torch.empty(n, dtype=torch.int32, device=self.device)
+        self._buf("action_out", action_out, torch.int32, (n,))
+        self._buf("path_len_out", path_len_out, torch.int32, (n,))
         self._check(N.lib().craft_teacher(self._h, _ptr(s), n, _ptr(t), _ptr(action_out),
                                           _ptr(path_len_out), self._stream()), "craft_teacher")
         return action_out, path_len_out

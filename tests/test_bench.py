@@ -1,0 +1,79 @@
+"""CPU tests of bench.py's host logic: the launch planner (any --steps/--warmup
+works with any --ticks-per-launch) and the --gpus / WORLD_SIZE check, which
+runs before any GPU call."""
+import types
+
+import pytest
+
+import bench
+
+
+@pytest.mark.parametrize("steps,k,expect", [
+    (20, 32, [20]),
+    (5, 32, [5]),
+    (1024, 32, [32] * 32),
+    (64, 32, [32, 32]),
+    (7, 32, [7]),
+    (0, 32, []),
+    (70, 32, [32, 32, 6]),
+    (3, 1, [1, 1, 1]),
+])
+def test_plan_launches(steps, k, expect):
+    plan = bench.plan_launches(steps, k)
+    assert plan == expect
+    assert sum(plan) == steps
+    assert all(1 <= x <= k for x in plan)
+
+
+def test_plan_rejects_bad_arguments():
+    with pytest.raises(ValueError):
+        bench.plan_launches(-1, 32)
+    with pytest.raises(ValueError):
+        bench.plan_launches(10, 0)
+
+
+def test_driver_command_line_parses():
+    a = bench.parse(["--gpus", "1", "--steps", "20", "--warmup", "5"])
+    assert (a.gpus, a.steps, a.warmup, a.ticks_per_launch) == (1, 20, 5, 32)
+    assert bench.plan_launches(a.steps, a.ticks_per_launch) == [20]
+    assert bench.plan_launches(a.warmup, a.ticks_per_launch) == [5]
+
+
+@pytest.mark.parametrize("argv", [["--steps", "0"], ["--gpus", "0"], ["--warmup", "-1"],
+                                  ["--ticks-per-launch", "0"], ["--tile", "48"]])
+def test_parse_rejects_before_gpu_work(argv):
+    with pytest.raises(SystemExit):
+        bench.parse(argv)
+
+
+def test_world_check():
+    a = types.SimpleNamespace(gpus=1)
+    assert bench.world_check(a, {}) == "run"
+    assert bench.world_check(a, {"WORLD_SIZE": "1"}) == "run"
+    a8 = types.SimpleNamespace(gpus=8)
+    assert bench.world_check(a8, {}) == "spawn"
+    assert bench.world_check(a8, {"WORLD_SIZE": "8"}) == "run"
+    msg = bench.world_check(a8, {"WORLD_SIZE": "2"})
+    assert msg not in ("run", "spawn") and "WORLD_SIZE=2" in msg
+
+
+def test_mismatched_world_size_exits_nonzero(monkeypatch, capsys):
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench.main(["--gpus", "2", "--steps", "20"]) == 2
+    assert "WORLD_SIZE=1" in capsys.readouterr().err
+
+
+def test_spawn_refuses_more_gpus_than_visible(monkeypatch, capsys):
+    """--gpus 2 on a box with fewer GPUs fails loudly instead of printing n_gpus 1."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    import torch
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert bench.main(["--gpus", "2", "--steps", "20"]) == 2
+    assert "only 1 GPU" in capsys.readouterr().err
+
+
+def test_bytes_per_env_step():
+    # 1754 B (w=3), 4505 B (w=5); the teacher adds 144 + 2 + 4 B
+    assert bench.bytes_per_env_step(12, 12, 3, 404) == 1754
+    assert bench.bytes_per_env_step(12, 12, 5, 1076) == 4505
+    assert bench.bytes_per_env_step(12, 12, 3, 404, teacher=True) == 1754 + 150

@@ -309,3 +309,29 @@ def test_language_teacher_matches_reference(golden, oracle_mod):
         assert [WORDS.index(w) for w in d] == fx["desc_seq"][i].tolist(), i
     for i in range(len(fx["instruct"])):
         assert [WORDS.index(w) for w in teacher.instruct(None, actions[:, i])] == fx["instruct"][i].tolist()
+
+
+# ---- the numpy CPU leg of bench.py's cpu_baseline --------------------------------------------
+@pytest.mark.parametrize("window", [3, 5])
+def test_numpy_restatement_matches_reference_rollout(golden, window):
+    """oracle/craft_numpy.py (the Python CPU comparator) replays the reference's own
+    100-tick random rollout (tests/golden/rollout_12x12_w3.npz) observation for
+    observation: step craft.py:332-424, features craft.py:296-330."""
+    from oracle.craft_numpy import NumpyWorld
+    g = golden(f"rollout_12x12_w{window}.npz")
+    _, _, tm, cfg = make_tables(world_for(12, window))
+    w = NumpyWorld(cfg)
+    batch = w.start([w.onehot(p) for p in g["pool"]], g["spec"])
+    seed = int(g["seed"][0])
+    obs_ticks = list(g["obs_ticks"])
+    for t in range(g["done"].shape[0]):
+        rec = []
+        w.tick(batch, 0, seed, t, rec)
+        obs, reward, done, success = rec[0]
+        np.testing.assert_array_equal(done, g["done"][t])
+        np.testing.assert_array_equal(success, g["success"][t])
+        np.testing.assert_array_equal(reward, g["reward"][t])
+        pos = np.asarray([s["pos"] for s in batch["states"]])
+        np.testing.assert_array_equal(pos, g["agent"][t][:, :2])
+        if t in obs_ticks:
+            np.testing.assert_array_equal(obs, g["obs"][obs_ticks.index(t)])
