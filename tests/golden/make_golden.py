@@ -633,9 +633,107 @@ def gen_language(w12_grids):
     print("language.npz", len(map1), "map entries;", os.path.getsize(os.path.join(OUT, "language.npz")))
 
 
+def gen_config1(T=100, seed=1):
+    """BASELINE configs[0]: one CraftWorld env on the first instance of the
+    regenerated craft_medium_train.json, a 100-step random rollout on the
+    reference's CPU worlds/craft.py.
+
+    The train split is regenerated with make_data.py's own functions and
+    RandomState(123) stream (make_data.py:154-238): 100 de-duplicated worlds,
+    then per world and per get/make task 20 distinct init positions
+    (random_free, keep_connected=False), then `config.random.shuffle` of the
+    worlds; train = the first 80.  The DemonstrationTeacher draws no random
+    numbers, so the demonstrations need not be computed to reach the shuffle;
+    the first instance's demonstration is computed by the reference's teacher.
+    Actions: hash_action(seed, 0, t), uniform over the 6 actions.  Recorded per
+    step t (the state after action t; row 0 of `pre_*` is the initial state):
+    pos, dir, inventory, grid (kind ids), features (uint8, exact) and
+    satisfies(task) for the instance's task."""
+    cfg, world = make_world()
+    tm = TaskManager(cfg)
+    fns = make_data_functions(world)
+    teacher = teachers.load(cfg)
+    ingredients = [world.cookbook.index[i] for i in ["wood", "grass", "iron"]]
+    grids = []
+    while len(grids) < world.N_WORLDS:
+        grid, _ = fns["sample_scenario"](world, ingredients, cfg)
+        if any((grid == g).all() for g in grids):
+            continue
+        grids.append(grid)
+    items, n_inst = [], 0
+    for grid in grids:
+        insts = []
+        for task in tm.tasks:
+            if task.goal_name not in ("get", "make"):
+                continue
+            poss, ids = [], []
+            while len(poss) < 20:
+                pos = fns["random_free"](world, grid, cfg.random, keep_connected=False)
+                if pos not in poss:
+                    n_inst += 1
+                    poss.append(pos)
+                    ids.append(n_inst)
+            insts.append((task, poss, ids))
+        items.append((grid, insts))
+    cfg.random.shuffle(items)
+    train = items[:world.N_WORLDS * 80 // 100]
+    grid, insts = train[0]
+    task, poss, ids = insts[0]
+    pos = poss[0]
+    task_id = [f"{t.goal_name}[{t.goal_arg}]" for t in tm.tasks].index(f"{task.goal_name}[{task.goal_arg}]")
+    # the reference demonstration of this instance (make_data.py:146-152)
+    state = world.init_state(grid, pos)
+    demo = [teacher(task, state)]
+    while demo[-1] != world.actions.STOP.index:
+        _, state = state.step(demo[-1])
+        demo.append(teacher(task, state))
+    assert state.satisfies(task)
+    # the 100-step random rollout
+    state = world.init_state(grid, pos)
+    rec = {k: [] for k in ("pos", "dir", "inv", "grid", "features", "satisfies")}
+
+    def record(st):
+        rec["pos"].append(st.pos)
+        rec["dir"].append(st.dir)
+        rec["inv"].append(np.asarray(st.inventory))
+        rec["grid"].append(onehot_to_ids(st.grid).reshape(-1))
+        f = st.features()
+        assert (f.astype(np.uint8) == f).all()
+        rec["features"].append(f.astype(np.uint8))
+        rec["satisfies"].append(int(bool(st.satisfies(task))))
+
+    record(state)
+    actions = [hash_action(seed, 0, t) for t in range(T)]
+    for a in actions:
+        r, state = state.step(a)
+        assert r == 0
+        record(state)
+    arrays = {
+        "train_grids": np.stack([onehot_to_ids(g).reshape(-1) for g, _ in train]).astype(np.uint8),
+        "train0_pos": np.asarray([p for _, ps, _ in insts for p in ps], dtype=np.int8).reshape(len(insts), 20, 2),
+        "train0_ids": np.asarray([i for _, _, ii in insts for i in ii], dtype=np.int32).reshape(len(insts), 20),
+        "task": np.asarray([task_id], dtype=np.int32),
+        "init_pos": np.asarray(pos, dtype=np.int32),
+        "demo": np.asarray(demo, dtype=np.int8),
+        "actions": np.asarray(actions, dtype=np.int8),
+        "pos": np.asarray(rec["pos"], dtype=np.int8),
+        "dir": np.asarray(rec["dir"], dtype=np.int8),
+        "inv": np.stack(rec["inv"]).astype(np.uint8),
+        "grid": np.stack(rec["grid"]).astype(np.uint8),
+        "features": np.stack(rec["features"]),
+        "satisfies": np.asarray(rec["satisfies"], dtype=np.int8),
+        "seed": np.asarray([seed]),
+    }
+    np.savez_compressed(os.path.join(OUT, "config1_train0.npz"), **arrays)
+    print("config1_train0.npz", task_id, pos, len(demo), os.path.getsize(os.path.join(OUT, "config1_train0.npz")))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["language"]:            # only the language-teacher fixture
         gen_language(np.load(os.path.join(OUT, "scenarios_seed123.npz"))["w12_grids"])
+        sys.exit(0)
+    if sys.argv[1:] == ["config1"]:             # only the configs[0] train-instance fixture
+        gen_config1()
         sys.exit(0)
     if sys.argv[1:] == ["imitation"]:           # only the do_rollout fixture
         gen_imitation(np.load(os.path.join(OUT, "scenarios_seed123.npz"))["w12_grids"])
@@ -650,3 +748,4 @@ if __name__ == "__main__":
     gen_rollout(sc["w12_grids"], 5, T=60, E=48, P=16, all_obs_ticks=None)
     gen_imitation(sc["w12_grids"])
     gen_language(sc["w12_grids"])
+    gen_config1()

@@ -223,3 +223,23 @@ def test_step_args_layout_matches_c(tmp_path):
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     want = [getattr(N.craft_step_args_t, f).offset for f in fields] + [ctypes.sizeof(N.craft_step_args_t)]
     assert got == want
+
+
+def test_config1_train_instance_regenerated(golden, oracle_mod):
+    """BASELINE configs[0]: the oracle's make_data restatement regenerates the
+    reference's craft_medium_train.json worlds and the first world's instance
+    positions and ids (tests/golden/config1_train0.npz, produced by the
+    reference's make_data.py functions, make_data.py:154-238)."""
+    from oracle.make_data_oracle import make_dataset
+    from psketch_amd.cookbook import generator_primitives
+    g = golden("config1_train0.npz")
+    params, cb, tm, cfg = make_tables("craft_medium")
+    data = make_dataset(params, cb, tm, oracle_mod.Oracle(cfg), generator_primitives(cb), seed=123)
+    train = data["train"]
+    np.testing.assert_array_equal(np.stack([it["grid"].reshape(-1) for it in train]), g["train_grids"])
+    tis = train[0]["task_instances"]
+    np.testing.assert_array_equal(np.asarray([ti["init_pos"] for ti in tis]), g["train0_pos"])
+    np.testing.assert_array_equal(np.asarray([[int(str(i).split("_")[-1]) for i in ti["ids"]] for ti in tis]),
+                                  g["train0_ids"])
+    assert tis[0]["task"] == int(g["task"][0])
+    assert list(tis[0]["ref_actions"][0]) == g["demo"].tolist()

@@ -335,3 +335,26 @@ def test_numpy_restatement_matches_reference_rollout(golden, window):
         np.testing.assert_array_equal(pos, g["agent"][t][:, :2])
         if t in obs_ticks:
             np.testing.assert_array_equal(obs, g["obs"][obs_ticks.index(t)])
+
+
+def test_oracle_config1_random_rollout(golden, oracle_mod):
+    """BASELINE configs[0]: the reference's 100-step random rollout of the first
+    craft_medium_train.json instance (tests/golden/config1_train0.npz), replayed
+    step by step through the oracle: pos, dir, inventory, grid, features and
+    satisfies after every step (craft.py:285-424)."""
+    g = golden("config1_train0.npz")
+    _, _, tm, cfg = make_tables("craft_medium")
+    o = oracle_mod.Oracle(cfg)
+    x, y = (int(v) for v in g["init_pos"])
+    env = o.env(g["grid"][0], x, y, 0)
+    task = int(g["task"][0])
+    for t in range(len(g["actions"]) + 1):
+        if t:
+            assert o.step(env, int(g["actions"][t - 1])) == 0
+        assert (int(env["x"][0]), int(env["y"][0])) == tuple(g["pos"][t])
+        assert int(env["dir"][0]) == g["dir"][t]
+        np.testing.assert_array_equal(env["inv"][0, :cfg.n_kinds], g["inv"][t])
+        np.testing.assert_array_equal(env["grid"][0, :64], g["grid"][t])
+        np.testing.assert_array_equal(o.features(env), g["features"][t].astype(np.float32))
+        assert o.satisfies(env, task) == g["satisfies"][t]
+    assert o.teacher(o.env(g["grid"][0], x, y, 0), task) == (0, int(g["demo"][0]))

@@ -14,7 +14,7 @@ timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"; ok $rc || exit $rc
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"; ok $rc || exit $rc
 fi
 
