@@ -14,7 +14,8 @@ one craft_step launch per tick instead.
 
 --workload teacher is configs[4]: every tick also runs the on-GPU
 DemonstrationTeacher (teachers/demonstration.py) for every env, the DAgger
-label of that tick's state.
+label of the next tick's state, fused into the tick's launch (craft_step_teach;
+--teacher-mode separate runs craft_teacher + craft_step as two launches).
 
 Inputs (scenario pool, env states) are resident in HBM before the timed region.
 Observations stream into a ring of R = 16 device buffers (1.7 GB, 6.6x the
@@ -74,6 +75,9 @@ def parse(argv=None):
     p.add_argument("--workload", choices=("rollout", "teacher"), default="rollout",
                    help="rollout: configs[2] (random rollout, full features); "
                         "teacher: configs[4] (+ the BFS DemonstrationTeacher label every tick)")
+    p.add_argument("--teacher-mode", choices=("fused", "separate"), default="fused",
+                   help="teacher workload: one craft_step_teach launch per tick, or craft_teacher "
+                        "then craft_step")
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--world", default="craft_medium_12x12")
     p.add_argument("--pool", type=int, default=1024)
@@ -93,6 +97,10 @@ def parse(argv=None):
     p.add_argument("--obs-only", action="store_true",
                    help="diagnostic: skip the reward/done/success rings (not a bench line)")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process-group backend for N > 1 (nccl = RCCL over xGMI)")
+    p.add_argument("--one-device", action="store_true",
+                   help="rehearsal: every rank on cuda:0 (a 1-GPU box; use --dist-backend gloo)")
     p.add_argument("--cpu-seconds", type=float, default=8.0,
                    help="wall seconds of each cpu_baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -134,7 +142,7 @@ def spawn_ranks(args, argv):
     process has not touched the GPU) and return its exit code."""
     import torch
     have = torch.cuda.device_count()          # counts devices without initialising HIP
-    if have < args.gpus:
+    if have < args.gpus and not args.one_device:
         print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
         return 2
     with socket.socket() as s:
@@ -214,9 +222,11 @@ def run(args):
     from psketch_amd import distributed as D
 
     rank, world_size, local_rank = D.world()
+    if args.one_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    D.init(device=dev)                        # RCCL process group when WORLD_SIZE > 1
+    D.init(device=dev, backend=args.dist_backend)   # RCCL process group when WORLD_SIZE > 1
 
     teacher = args.workload == "teacher"
     K = 1 if teacher else args.ticks_per_launch
@@ -252,10 +262,15 @@ def run(args):
         if K == 1:
             for _ in range(k):
                 r = tick % R
-                if teacher:
-                    sim.teacher(action_out=labels[r])      # DAgger label of the tick's state
-                sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r], done=done[r],
-                         success=success[r])
+                if teacher and args.teacher_mode == "fused":
+                    # the tick, then the DAgger label of every env's new state, one launch
+                    sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r], done=done[r],
+                             success=success[r], labels=labels[r])
+                else:
+                    if teacher:
+                        sim.teacher(action_out=labels[r])  # DAgger label of the tick's state
+                    sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r],
+                             done=done[r], success=success[r])
                 tick += 1
         else:
             if args.obs_only:
@@ -314,7 +329,10 @@ def run(args):
         else:
             tile, _ = sim.tile_shape()
             kname = f"tile_kernel<{win}, MODE_TICK, {tile}>"
-            if teacher:
+            if teacher and args.teacher_mode == "fused":
+                nw = (sim.width * sim.height + 31) // 32
+                kname = f"tile_kernel<{win}, MODE_TICK, 64, 4, {nw}> (craft_step_teach)"
+            elif teacher:
                 kname += " + teacher_kernel"
             shape = {"tile": tile}
         achieved = bps * n * k_eff / (kernel_ms * 1e-3) / 1e9
@@ -322,6 +340,8 @@ def run(args):
             "teacher_labels_full_features" if teacher else "random_rollout_full_features")
         if K > 1:
             workload += f"_K{K}"
+        if teacher:
+            workload += "_" + args.teacher_mode
         traffic = None
         tpath = args.traffic or os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(tpath):

@@ -260,6 +260,17 @@ typedef struct {
 } craft_step_args_t;
 int craft_step_ex(craft_sim_t* sim, const craft_step_args_t* args, void* stream);
 
+/* craft_step_ex fused with craft_teacher on every slot's NEW state (its own task),
+ * in one launch: label_out (device int32[n_envs]) receives
+ * DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) of each slot
+ * after the tick — the ref_actions of the next tick of ImitationTrainer.do_rollout
+ * (trainers/imitation.py:47-55): -1 for a slot the tick left frozen, -2 (and
+ * CRAFT_ETEACHER latched) where the reference raises.  Identical to craft_step_ex
+ * followed by craft_teacher(slots NULL, tasks NULL), but the teacher reads the
+ * grid rows the tick holds on chip instead of rebuilding them from HBM, and its
+ * BFS overlaps the observation stores (config 5: a teacher label every tick). */
+int craft_step_teach(craft_sim_t* sim, const craft_step_args_t* args, int32_t* label_out, void* stream);
+
 /* n_ticks consecutive craft_step ticks (tick0, tick0+1, ...) in one launch, with
  * results identical to n_ticks craft_step calls: each workgroup keeps its envs
  * on chip between ticks, so the per-tick prologue overlaps other workgroups'

@@ -121,6 +121,7 @@ SIGNATURES = {
     "craft_reset": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "craft_step": (_i32, [_vp, _vp, _u64, _i64, _u32, _vp, _vp, _vp, _vp, _vp]),
     "craft_step_ex": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp]),
+    "craft_step_teach": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp, _vp]),
     "craft_rollout": (_i32, [_vp, _vp, _u64, _i64, _i32, _u32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "craft_stats": (_i32, [_vp, _vp, _i32, _vp]),
     "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),

@@ -124,6 +124,7 @@ struct TileArgs {
   int32_t* rec;
   int32_t* any_live;
   int8_t* code;            // transition codes (craft_step_ex, craft_transition)
+  int32_t* label;          // craft_step_teach: teacher label of every env's new state
 };
 
 struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
@@ -140,6 +141,7 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   int32_t chunk;           // ticks per work unit
   unsigned long long* queue;   // work-unit counter, zeroed before the launch
   uint32_t* tile_done;     // per tile: chunks completed in this launch, zeroed before the launch
+  int32_t flat;            // split kernel, one unit per tile: one continuous pipeline (no queue)
 };
 
 struct ScenarioArgs {      // craft_pool_generate

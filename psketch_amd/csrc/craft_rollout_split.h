@@ -1,23 +1,35 @@
 // craft_rollout_split.h — craft_rollout for 16- and 32-env tiles: the producer
 // work of a tick split over two waves.
 //
-// Small tiles store faster (store-pattern tables: 16-row tiles reach
-// ~15 us per tick against ~18.5 for 64-row tiles), but every tile needs its own
-// transition latency chain, so one wave doing both the transition and the
-// scatter cannot keep up.  Here:
-//   wave 0        C(q+1): the transitions (one lane per env);
-//   wave 1        D(q):   the observation scatter of the tick before (64 / TILE
-//                         lanes per env) into LDS row buffer q & 1;
-//   waves 2..     E(q-1): stream the rows of the tick before that to HBM and
+// Small tiles need their own transition latency chain each, so one wave doing
+// both the transition and the scatter cannot keep up.  Here:
+//   wave 0        C(j+1): the transitions (one lane per env);
+//   wave 1        D(j):   the observation scatter of the item before (64 / TILE
+//                         lanes per env) into LDS row buffer j & 1;
+//   waves 2..     E(j-1): stream the rows of the item before that to HBM and
 //                         clear them.
-// One workgroup barrier per tick.  C(q+1) and D(q) run at the same time, so the
-// env state is double-buffered by tick parity: grid rows and inventory rows of
-// tick q live in buffer q & 1.  C(q+1) first brings its buffer (which holds tick
-// q-1) up to tick q — a tick changes at most one cell per env (grab, bridge,
-// axe) or restarts the episode, recorded in `chg` — and copies the inventory,
-// then runs the tick on it.  Everything else (work units, hand-off, outputs,
-// statistics) is as in craft_rollout.h, and the results are identical (the same
-// tests run both kernels).
+// One workgroup barrier per interval.  An "item" is one tick of one tile.
+//
+// Continuous pipeline.  When a launch is one work unit per tile (the default:
+// no chunked hand-offs), a workgroup's items are all ticks of its first tile,
+// then all ticks of its next tile, ... (tiles b, b + G, b + 2G for workgroup b
+// of G), and the pipeline runs straight through tile changes: in the interval
+// where D and E still work on the previous tile's last ticks, wave 0 publishes
+// that tile's state, loads the next tile and runs its first tick.  The pipeline
+// fills once and drains once per launch instead of once per tile
+// (the launch's fixed cost).  Chunked launches (craft_sim_tune_rollout
+// chunk > 0) keep one fill and drain per unit, because a unit may have to wait
+// for its tile's previous chunk on another workgroup.
+//
+// Parity.  C(j+1) and D(j) run at the same time, so the env state is
+// double-buffered by item parity: grid rows and inventory rows of item j live in
+// buffer j & 1.  A tick changes at most one cell per env (grab, bridge, axe) or
+// restarts the episode, recorded in `chg`; C(j+1) first brings its buffer (two
+// items old) up to date from that record and copies the inventory, then runs the
+// tick.  A freshly loaded tile fills only its first item's buffer; its second
+// item copies the whole row across.  Everything else (outputs, statistics) is as
+// in craft_rollout.h, and the results are identical (the same tests run both
+// kernels).
 #pragma once
 #include "craft_obs.h"
 
@@ -25,11 +37,11 @@ namespace craft {
 
 // LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation
 // rows [2][up16(TILE*F)] | inventory rows [2][TILE][36] | agent words [2][TILE] |
-// task table [64] u16 | recipe words [16][3] | control words [4].
+// task table [64] u16 | recipe words [16][3] | control words [4] | item words [4][2].
 __host__ __device__ inline int split_lds_bytes(int tile, int GS, int F) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   return up16(3 * tile * GS) + 2 * up16(tile * F) + 2 * tile * kInvStride + 2 * tile * 4 +
-         CRAFT_MAX_TASKS * 2 + CRAFT_MAX_RECIPES * 12 + 16;
+         CRAFT_MAX_TASKS * 2 + CRAFT_MAX_RECIPES * 12 + 16 + 32;
 }
 
 template <int WIN, int TILE, int NT, int FMT, int WPE, bool GIVEN>
@@ -39,7 +51,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   constexpr int P = 64 / TILE;                            // scatter lanes per env
   auto up16 = [](int x) { return (x + 15) & ~15; };
   const int GS = v.GS, F = v.F;
-  uint8_t* s_grid = smem;                                 // [2][TILE][GS] by tick parity
+  uint8_t* s_grid = smem;                                 // [2][TILE][GS] by item parity
   uint8_t* s_pristine = smem + 2 * TILE * GS;             // [TILE][GS] pool[scenario]
   const int obs_buf = up16(TILE * F);
   uint8_t* s_obs = smem + up16(3 * TILE * GS);            // [2][obs_buf]
@@ -48,6 +60,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   uint16_t* s_task = reinterpret_cast<uint16_t*>(s_agent + 2 * TILE);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(s_task + CRAFT_MAX_TASKS);
   uint32_t* s_ctrl = s_rc + CRAFT_MAX_RECIPES * 3;
+  uint32_t* s_item = s_ctrl + 4;                          // [4][2]: item j -> {tile + 1 (0 = none), tick}
 
   const int tid = threadIdx.x;
   const int64_t n = v.n_envs;
@@ -65,16 +78,17 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   uint32_t clr_prev = 0;     // the episode's clears before a restart (for the other buffer)
   uint32_t chg = 0;          // what the last C did to its buffer: 0 nothing, 1 + cell cleared, kRestart
   constexpr uint32_t kRestart = 0x80000000u;
+  int sync = 0;              // how C brings its buffer up to date: 0 loaded, 1 whole copy, 2 from chg
   bool live = false;
   int64_t slot = 0;
   const uint32_t* pw = reinterpret_cast<const uint32_t*>(s_pristine + tid * GS);
   const uint8_t* pr = s_pristine + tid * GS;
-  auto grid_of = [&](int q) { return s_grid + (q & 1) * TILE * GS + tid * GS; };
-  auto inv_of = [&](int q) { return s_inv + (q & 1) * TILE * kInvStride + tid * kInvStride; };
+  auto grid_of = [&](int p) __attribute__((always_inline)) { return s_grid + (p & 1) * TILE * GS + tid * GS; };
+  auto inv_of = [&](int p) __attribute__((always_inline)) { return s_inv + (p & 1) * TILE * kInvStride + tid * kInvStride; };
   uint32_t n_succ = 0, n_end = 0, n_step = 0;
 
   // restore the cells of `cl` (or the whole row) of grid row g from the pristine row
-  auto restore = [&](uint8_t* g, uint32_t cl) {
+  auto restore = [&](uint8_t* g, uint32_t cl) __attribute__((always_inline)) {
     if (cl >> 31) {
       uint32_t* gw = reinterpret_cast<uint32_t*>(g);
       for (int q0 = 0; q0 < (v.CS >> 2); q0 += 12) {
@@ -96,26 +110,40 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     }
   };
 
-  // ---- C(q), local tick q = k - k0: tick k on buffer q & 1 (trainers/imitation.py:59-73) -------
-  auto tick_c = [&](int k, int q) {
+  // ---- C: tick k on buffer p (trainers/imitation.py:59-73) -------------------------------------
+  auto tick_c = [&](int k, int p) __attribute__((always_inline)) {
     const int64_t tick = a.tick0 + k;
     const int64_t r = tick % a.ring;
     int d = 0, succ = -1, counted = 0;
-    uint8_t* g = grid_of(q);
-    uint8_t* iv = inv_of(q);
+    uint8_t* g = grid_of(p);
+    uint8_t* iv = inv_of(p);
     s = unpack_state(st);
     if (live) {
-      // bring this buffer (tick q-2) up to tick q-1: the other buffer's last change, inventory copy
-      if (q > 0) {
+      // bring this buffer up to the other buffer's state: whole row after a load, else its last change
+      if (sync == 1) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(grid_of(p ^ 1));
+        uint32_t* gw = reinterpret_cast<uint32_t*>(g);
+        for (int q0 = 0; q0 < (v.CS >> 2); q0 += 12) {
+          uint32_t w[12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) w[j] = q0 + j < (v.CS >> 2) ? src[q0 + j] : 0u;
+#pragma unroll
+          for (int j = 0; j < 12; ++j)
+            if (q0 + j < (v.CS >> 2)) gw[q0 + j] = w[j];
+        }
+      } else if (sync == 2) {
         if (chg == kRestart) restore(g, clr_prev);
         else if (chg) g[chg - 1] = 0;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(inv_of(q - 1));
+      }
+      if (sync) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(inv_of(p ^ 1));
         uint32_t w[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) w[i] = src[i];
 #pragma unroll
         for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(iv)[i] = w[i];
       }
+      sync = sync ? 2 : 1;
       chg = 0;
       int act;
       if (GIVEN) {
@@ -180,22 +208,144 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     n_succ += (uint32_t)__popcll(bs);
     n_end += (uint32_t)__popcll(be);
     n_step += (uint32_t)__popcll(bt);
-    s_agent[(q & 1) * TILE + tid] =
+    s_agent[(p & 1) * TILE + tid] =
         live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
   };
 
-  // ---- D(q) on wave 1: lane l scatters part l / TILE of env l % TILE --------------------------
-  auto scatter_d = [&](int q, int nE) {
+  // ---- A: lanes < TILE of wave 0 take over tile t into buffer p (state, pool row, clears) -----
+  auto load_tile = [&](int t, int p) __attribute__((always_inline)) {
+    const int64_t env0 = (int64_t)t * TILE;
+    const int nE = (int)min((int64_t)TILE, n - env0);
+    slot = env0 + tid;
+    live = tid < nE;
+    uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t ivr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) {
+      st = v.state[slot];
+      init_word = v.init[slot];
+      const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
+      const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+      ivr[0] = i0.x; ivr[1] = i0.y; ivr[2] = i0.z; ivr[3] = i0.w;
+      ivr[4] = i1.x; ivr[5] = i1.y; ivr[6] = i1.z; ivr[7] = i1.w;
+      m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
+      m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
+      s = unpack_state(st);
+      if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
+        latch_error(v.err, CRAFT_EINVAL, slot);
+        live = false;
+      }
+    }
+    chg = 0;
+    clr = 0;
+    clr_prev = 0;
+    sync = 0;
+    if (live) {
+      task_word = s_task[s.task];
+      // pool[scenario] -> the pristine row and grid buffer p; inventory -> buffer p
+      uint32_t* g0 = reinterpret_cast<uint32_t*>(grid_of(p));
+      uint32_t* pwm = reinterpret_cast<uint32_t*>(s_pristine + tid * GS);
+      const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
+      const int nchunk = v.CS >> 4;
+      for (int q0 = 0; q0 < nchunk; q0 += 4) {
+        uint4 cq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < nchunk) cq[j] = src[q0 + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (q0 + j < nchunk) {
+            const int q = 4 * (q0 + j);
+            pwm[q + 0] = g0[q + 0] = cq[j].x;
+            pwm[q + 1] = g0[q + 1] = cq[j].y;
+            pwm[q + 2] = g0[q + 2] = cq[j].z;
+            pwm[q + 3] = g0[q + 3] = cq[j].w;
+          }
+      }
+      uint32_t* iv0 = reinterpret_cast<uint32_t*>(inv_of(p));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) iv0[i] = ivr[i];
+      uint8_t* b0 = grid_of(p);
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {                     // cells cleared this episode
+        uint32_t mm = m[w];
+        while (mm) {
+          const int cc = w * 32 + __ffs(mm) - 1;
+          b0[cc] = 0;
+          const uint32_t nc = (clr >> 24) & 3;
+          clr = (clr >> 31) ? clr
+              : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)cc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
+          mm &= mm - 1;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  // ---- the tile's state back to HBM from buffer p (its last item); the mask is rebuilt from
+  // the rows: cells are only ever cleared, so mask = {c : pristine[c] != 0 and grid[c] == 0} ---
+  auto publish = [&](int p, bool sc1) __attribute__((always_inline)) {
+    const uint32_t* gw = reinterpret_cast<const uint32_t*>(grid_of(p));
+    const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of(p));
+    uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int q = 0; q < (v.CS >> 2); ++q) {
+      const uint32_t pp = pw[q], cc = gw[q];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const bool cleared = ((pp >> (8 * b)) & 0xffu) != 0 && ((cc >> (8 * b)) & 0xffu) == 0;
+        const int cell = 4 * q + b;
+        if (cleared) m[cell >> 5] |= 1u << (cell & 31);
+      }
+    }
+    if (sc1) {
+      // write-through (sc1) stores: the hand-off form of MI355X_MICROARCH.md "Valid forms"
+      // ({sc1 stores} -> every storing wave's s_waitcnt vmcnt(0) -> one lane's flag)
+      typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t inv_r = __builtin_amdgcn_make_buffer_rsrc(v.inv, 0, 0x7fffffff, 0x00020000);
+      const __amdgpu_buffer_rsrc_t msk_r = __builtin_amdgcn_make_buffer_rsrc(v.mask, 0, 0x7fffffff, 0x00020000);
+      const int off = (int)(slot * 32);
+      __hip_atomic_store((gu64*)(v.state + slot), (unsigned long long)st, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[0], ivw[1], ivw[2], ivw[3]}, inv_r, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[4], ivw[5], ivw[6], ivw[7]}, inv_r, off + 16, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{m[0], m[1], m[2], m[3]}, msk_r, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{m[4], m[5], m[6], m[7]}, msk_r, off + 16, 0, 16);
+    } else {
+      v.state[slot] = st;
+      v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+      v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
+      v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
+      v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
+    }
+  };
+
+  // ---- D on wave 1: lane l scatters part l / TILE of env l % TILE of the item in buffer p ----
+  auto scatter_d = [&](int p, int nE) __attribute__((always_inline)) {
     const int l = tid - 64, e = l % TILE;
-    const uint32_t ag = s_agent[(q & 1) * TILE + e];
+    const uint32_t ag = s_agent[(p & 1) * TILE + e];
 #ifdef CRAFT_ABL_NOD
     if (false)
 #else
     if (e < nE && ag)
 #endif
-      scatter_env_part<WIN, P>(v, s_grid + (q & 1) * TILE * GS + e * GS,
-                               s_inv + (q & 1) * TILE * kInvStride + e * kInvStride, ag,
-                               s_obs + (q & 1) * obs_buf + e * F, l / TILE);
+      scatter_env_part<WIN, P>(v, s_grid + (p & 1) * TILE * GS + e * GS,
+                               s_inv + (p & 1) * TILE * kInvStride + e * kInvStride, ag,
+                               s_obs + (p & 1) * obs_buf + e * F, l / TILE);
+  };
+
+  // ---- E on waves 2..: stream tick k of tile t from buffer p to its ring slot ------------------
+  auto stream_e = [&](int p, int t, int k) __attribute__((always_inline)) {
+    const int64_t env0 = (int64_t)t * TILE;
+    const int nE = (int)min((int64_t)TILE, n - env0);
+    const int64_t r = (a.tick0 + k) % a.ring;
+    void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
+#ifndef CRAFT_ABL_NOE
+    stream_obs<FMT, NT - 128, true>(s_obs + (p & 1) * obs_buf, out, env0, F, nE, v.obs_policy, tid - 128);
+#else
+    (void)out;
+    (void)nE;
+#endif
   };
 
   // ---- once per workgroup: task table, cleared observation rows --------------------------------
@@ -206,193 +356,165 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     for (int i = tid; i < (2 * obs_buf >> 4); i += NT) z[i] = make_uint4(0, 0, 0, 0);
   }
 
-  for (;;) {
-    if (tid == 0) s_ctrl[0] = (uint32_t)atomicAdd(a.queue, 1ull);
-    __syncthreads();                                    // also: s_task / rows ready
-    const uint32_t u = s_ctrl[0];
-    if (u >= n_units) break;                            // workgroup-uniform exit
-    const int t = (int)(u % (uint32_t)n_tiles), c = (int)(u / (uint32_t)n_tiles);
-    const int k0 = c * a.chunk, k1 = min(a.n_ticks, k0 + a.chunk);
-    const int nq = k1 - k0;
-    const int64_t env0 = (int64_t)t * TILE;
-    const int nE = (int)min((int64_t)TILE, n - env0);
-
-    // ---- A: wave 0 takes over the tile (after its previous chunk is published) ----------------
-    if (tid < 64) {
-      if (c > 0) {
-        bool ok = true;
-        if (tid == 0) {
-          const gu32* f = (const gu32*)(a.tile_done + t);
-          for (uint32_t spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)c;) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 26)) { ok = false; break; }   // bounded: never hang the GPU
-          }
-          if (!ok) latch_error(v.err, CRAFT_EINVARIANT, env0);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-      if (tid < TILE) {
-        slot = env0 + tid;
-        live = tid < nE;
-        uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        uint32_t ivr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (live) {
-          st = v.state[slot];
-          init_word = v.init[slot];
-          const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
-          const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
-          ivr[0] = i0.x; ivr[1] = i0.y; ivr[2] = i0.z; ivr[3] = i0.w;
-          ivr[4] = i1.x; ivr[5] = i1.y; ivr[6] = i1.z; ivr[7] = i1.w;
-          m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
-          m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
-          s = unpack_state(st);
-          if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
-            latch_error(v.err, CRAFT_EINVAL, slot);
-            live = false;
-          }
-        }
-        chg = 0;
-        clr = 0;
-        clr_prev = 0;
-        if (live) {
-          task_word = s_task[s.task];
-          // pool[scenario] -> the pristine row and both grid buffers; inventory -> both buffers
-          uint32_t* g0 = reinterpret_cast<uint32_t*>(s_grid + tid * GS);
-          uint32_t* g1 = reinterpret_cast<uint32_t*>(s_grid + TILE * GS + tid * GS);
-          uint32_t* pwm = reinterpret_cast<uint32_t*>(s_pristine + tid * GS);
-          const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
-          const int nchunk = v.CS >> 4;
-          for (int q0 = 0; q0 < nchunk; q0 += 4) {
-            uint4 cq[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (q0 + j < nchunk) cq[j] = src[q0 + j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (q0 + j < nchunk) {
-                const int q = 4 * (q0 + j);
-                pwm[q + 0] = g0[q + 0] = g1[q + 0] = cq[j].x;
-                pwm[q + 1] = g0[q + 1] = g1[q + 1] = cq[j].y;
-                pwm[q + 2] = g0[q + 2] = g1[q + 2] = cq[j].z;
-                pwm[q + 3] = g0[q + 3] = g1[q + 3] = cq[j].w;
-              }
-          }
-          uint32_t* iv0 = reinterpret_cast<uint32_t*>(s_inv + tid * kInvStride);
-          uint32_t* iv1 = reinterpret_cast<uint32_t*>(s_inv + TILE * kInvStride + tid * kInvStride);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) iv0[i] = iv1[i] = ivr[i];
-          uint8_t* b0 = s_grid + tid * GS;
-          uint8_t* b1 = s_grid + TILE * GS + tid * GS;
-#pragma unroll
-          for (int w = 0; w < 8; ++w) {                 // cells cleared this episode
-            uint32_t mm = m[w];
-            while (mm) {
-              const int cc = w * 32 + __ffs(mm) - 1;
-              b0[cc] = 0;
-              b1[cc] = 0;
-              const uint32_t nc = (clr >> 24) & 3;
-              clr = (clr >> 31) ? clr
-                  : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)cc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
-              mm &= mm - 1;
-            }
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        tick_c(k0, 0);                                  // C(0) -> buffer 0
-      }
-    }
-
-    // ---- the pipeline: interval i runs C(i+1) | D(i) | E(i-1), one barrier each -------------
-    if (!want_obs) {
-      if (tid < TILE)
-        for (int q = 1; q < nq; ++q) tick_c(k0 + q, q);
-    } else {
-      __syncthreads();                                  // C(0) complete
-      if (tid < 64) {
-        for (int i = 0; i <= nq; ++i) {
-          if (tid < TILE && i + 1 < nq) tick_c(k0 + i + 1, i + 1);
-          __syncthreads();
-        }
-      } else if (tid < 128) {
-        for (int i = 0; i <= nq; ++i) {
-          if (i < nq) scatter_d(i, nE);
-          __syncthreads();
-        }
-      } else {
-        const int et = tid - 128;
-        for (int i = 0; i <= nq; ++i) {
-          if (i >= 1) {
-            const int q = i - 1;
-            const int64_t r = (a.tick0 + k0 + q) % a.ring;
-            void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
-#ifndef CRAFT_ABL_NOE
-            stream_obs<FMT, NT - 128, true>(s_obs + (q & 1) * obs_buf, out, env0, F, nE,
-                                            v.obs_policy, et);
+  if (a.flat && n_chunks == 1 && want_obs) {
+    // ---- continuous pipeline: tiles b, b + G, ... of this workgroup, all ticks each ----------
+#ifdef CRAFT_STAMPS
+    // diagnostic build only: per-role totals in s_memrealtime ticks (10 ns) -> stamps[block][8]:
+    // 0 start, 1 wave 0 in produce, 2 wave 0 at the barrier, 3 wave 1 in D, 4 wave 1 at the
+    // barrier, 5 wave 2 in E, 6 end, 7 wave 0 in tile switches (publish + load)
+    unsigned long long t_beg = __builtin_amdgcn_s_memrealtime(), acc_work = 0, acc_wait = 0, acc_sw = 0;
+#define SPLIT_NOW() __builtin_amdgcn_s_memrealtime()
 #else
-            (void)out;
+#define SPLIT_NOW() 0ull
+    unsigned long long acc_work = 0, acc_wait = 0, acc_sw = 0;
 #endif
-          }
-          __syncthreads();
+    // wave-uniform state of wave 0: the tile in progress and its next tick
+    int cur_t = -1, cur_k = 0, next_j = 0;
+    auto produce = [&](int j) __attribute__((always_inline)) {                         // wave 0: item j into buffer j & 1
+      if (cur_t != -2 && (cur_t < 0 || cur_k == a.n_ticks)) {
+        const unsigned long long s0 = SPLIT_NOW();
+        if (cur_t >= 0 && tid < TILE && live) publish((j - 1) & 1, false);
+        const int t = (int)blockIdx.x + next_j * (int)gridDim.x;
+        ++next_j;
+        if (t < n_tiles) {
+          cur_t = t;
+          cur_k = 0;
+          if (tid < TILE) load_tile(t, j & 1);
+        } else {
+          cur_t = -2;                                   // no tile left: the pipeline drains
         }
+        acc_sw += SPLIT_NOW() - s0;
       }
-    }
-
-    // ---- publish the tile for the unit (t, c + 1) (as craft_rollout.h) ---------------------------
-    const bool state_only = a.ring >= a.n_ticks;
-    const bool handoff = c + 1 < n_chunks;
-    if (tid < TILE && live) {
-      const int ql = nq - 1;                            // the buffer of the last tick
-      const uint32_t* gw = reinterpret_cast<const uint32_t*>(grid_of(ql));
-      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of(ql));
-      uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int q = 0; q < (v.CS >> 2); ++q) {
-        const uint32_t p = pw[q], cc = gw[q];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const bool cleared = ((p >> (8 * b)) & 0xffu) != 0 && ((cc >> (8 * b)) & 0xffu) == 0;
-          const int cell = 4 * q + b;
-          if (cleared) m[cell >> 5] |= 1u << (cell & 31);
-        }
+      const bool have = cur_t >= 0;
+      if (have && tid < TILE) tick_c(cur_k, j & 1);
+      if (tid == 0) {
+        s_item[2 * (j & 3)] = have ? (uint32_t)cur_t + 1u : 0u;
+        s_item[2 * (j & 3) + 1] = (uint32_t)cur_k;
       }
-      if (handoff && state_only) {
-        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-        const __amdgpu_buffer_rsrc_t inv_r = __builtin_amdgcn_make_buffer_rsrc(v.inv, 0, 0x7fffffff, 0x00020000);
-        const __amdgpu_buffer_rsrc_t msk_r = __builtin_amdgcn_make_buffer_rsrc(v.mask, 0, 0x7fffffff, 0x00020000);
-        const int off = (int)(slot * 32);
-        __hip_atomic_store((gu64*)(v.state + slot), (unsigned long long)st, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[0], ivw[1], ivw[2], ivw[3]}, inv_r, off, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(u4v{ivw[4], ivw[5], ivw[6], ivw[7]}, inv_r, off + 16, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(u4v{m[0], m[1], m[2], m[3]}, msk_r, off, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(u4v{m[4], m[5], m[6], m[7]}, msk_r, off + 16, 0, 16);
-      } else {
-        v.state[slot] = st;
-        v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
-        v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
-        v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
-        v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
-      }
-    }
-    if (handoff && state_only) {
+      if (have) ++cur_k;
+    };
+    if (tid < 64) produce(0);
+    __syncthreads();
+    for (int i = 0;; ++i) {                             // interval i: C(i+1) | D(i) | E(i-1)
+      const unsigned long long w0 = SPLIT_NOW();
       if (tid < 64) {
+        produce(i + 1);
+      } else if (tid < 128) {
+        const uint32_t t1 = s_item[2 * (i & 3)];
+        if (t1) scatter_d(i & 1, (int)min((int64_t)TILE, n - (int64_t)(t1 - 1) * TILE));
+      } else if (i >= 1) {
+        const uint32_t t1 = s_item[2 * ((i - 1) & 3)];
+        if (t1) stream_e((i - 1) & 1, (int)t1 - 1, (int)s_item[2 * ((i - 1) & 3) + 1]);
+      }
+      const unsigned long long w1 = SPLIT_NOW();
+      __syncthreads();
+      acc_work += w1 - w0;
+      acc_wait += SPLIT_NOW() - w1;
+      if (s_item[2 * (i & 3)] == 0) break;              // item i does not exist: all work is done
+    }
+#ifdef CRAFT_STAMPS
+    if (v.stamps) {
+      uint64_t* row = v.stamps + 8 * (int64_t)blockIdx.x;
+      if (tid == 0) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        row[0] = t_beg; row[1] = acc_work; row[2] = acc_wait; row[6] = SPLIT_NOW(); row[7] = acc_sw;
+        (void)xcc;
+      } else if (tid == 64) {
+        row[3] = acc_work; row[4] = acc_wait;
+      } else if (tid == 128) {
+        row[5] = acc_work;
+      }
+    }
+#endif
+    (void)acc_work;
+    (void)acc_wait;
+    (void)acc_sw;
+#undef SPLIT_NOW
+  } else {
+    // ---- work units (tile t, chunk c) from the queue, one pipeline fill and drain each --------
+    for (;;) {
+      if (tid == 0) s_ctrl[0] = (uint32_t)atomicAdd(a.queue, 1ull);
+      __syncthreads();                                  // also: s_task / rows ready
+      const uint32_t u = s_ctrl[0];
+      if (u >= n_units) break;                          // workgroup-uniform exit
+      const int t = (int)(u % (uint32_t)n_tiles), c = (int)(u / (uint32_t)n_tiles);
+      const int k0 = c * a.chunk, k1 = min(a.n_ticks, k0 + a.chunk);
+      const int nq = k1 - k0;
+      const int64_t env0 = (int64_t)t * TILE;
+      const int nE = (int)min((int64_t)TILE, n - env0);
+
+      // A: wave 0 takes over the tile (after its previous chunk is published)
+      if (tid < 64) {
+        if (c > 0) {
+          bool ok = true;
+          if (tid == 0) {
+            const gu32* f = (const gu32*)(a.tile_done + t);
+            for (uint32_t spins = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)c;) {
+              __builtin_amdgcn_s_sleep(2);
+              if (++spins > (1u << 26)) { ok = false; break; }   // bounded: never hang the GPU
+            }
+            if (!ok) latch_error(v.err, CRAFT_EINVARIANT, env0);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        if (tid < TILE) {
+          load_tile(t, 0);
+          tick_c(k0, 0);                                // C(0) -> buffer 0
+        }
+      }
+
+      // the pipeline: interval i runs C(i+1) | D(i) | E(i-1), one barrier each
+      if (!want_obs) {
+        if (tid < TILE)
+          for (int q = 1; q < nq; ++q) tick_c(k0 + q, q);
+      } else {
+        __syncthreads();                                // C(0) complete
+        if (tid < 64) {
+          for (int i = 0; i <= nq; ++i) {
+            if (tid < TILE && i + 1 < nq) tick_c(k0 + i + 1, i + 1);
+            __syncthreads();
+          }
+        } else if (tid < 128) {
+          for (int i = 0; i <= nq; ++i) {
+            if (i < nq) scatter_d(i, nE);
+            __syncthreads();
+          }
+        } else {
+          for (int i = 0; i <= nq; ++i) {
+            if (i >= 1) stream_e(i - 1, t, k0 + i - 1);
+            __syncthreads();
+          }
+        }
+      }
+
+      // publish the tile for the unit (t, c + 1) (as craft_rollout.h).  Without observation
+      // ring reuse inside the launch (ring >= n_ticks) only wave 0's state stores are handed
+      // over: they go write-through (sc1) and lane 0 raises the flag after the wave's own
+      // drain; otherwise every wave drains and lane 0 releases at agent scope first, so a
+      // later chunk rewriting the same ring slot from another XCD lands last.
+      const bool state_only = a.ring >= a.n_ticks;
+      const bool handoff = c + 1 < n_chunks;
+      if (tid < TILE && live) publish(nq - 1, handoff && state_only);
+      if (handoff && state_only) {
+        if (tid < 64) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (tid == 0)
+            __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else if (handoff) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (tid == 0)
+        __syncthreads();
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
-    } else if (handoff) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
+      __syncthreads();                                  // s_ctrl and the LDS rows are reused
     }
-    __syncthreads();                                    // s_ctrl and the LDS rows are reused
   }
 
   if (tid == 0) {

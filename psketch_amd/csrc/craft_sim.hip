@@ -2,6 +2,7 @@
 // scenario pool, launches, state I/O and episode statistics.
 // Kernels: craft_tile.hip (tick / transition / observe / reset), craft_rollout.hip
 // (multi-tick), craft_teacher.hip, craft_scenarios.hip (pool generation).
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -17,6 +18,8 @@ hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const 
 hipError_t launch_rollout(int win, int tile, int threads, const SimView& v, const RolloutArgs& a, size_t lds,
                           hipStream_t st);
 hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t st);
+hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
+                             hipStream_t st);
 
 namespace {
 
@@ -558,12 +561,12 @@ int craft_step(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, int
   return craft_step_ex(s, &x, stream);
 }
 
-int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
-  if (!s || !x) return CRAFT_EINVAL;
+namespace {
+int step_args(craft_sim_t* s, const craft_step_args_t* x, TileArgs& a) {
   if (x->obs && !aligned16(x->obs)) return fail(s, CRAFT_EINVAL, "craft_step: obs must be 16-byte aligned");
   if (x->behavior_clone && !x->ref_actions)
     return fail(s, CRAFT_EINVAL, "craft_step_ex: behavior_clone needs ref_actions");
-  TileArgs a{};
+  a = TileArgs{};
   a.actions = x->actions;
   a.seed = x->action_seed;
   a.tick = x->tick;
@@ -578,6 +581,33 @@ int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
   a.rec = x->action_record;
   a.any_live = x->any_live;
   a.code = x->transition_code;
+  return CRAFT_OK;
+}
+}  // namespace
+
+int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_out, void* stream) {
+  if (!s || !x || !label_out) return CRAFT_EINVAL;
+  if (4 * s->view.C > 1000)
+    return fail(s, CRAFT_EINVAL, "craft_step_teach: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
+  TileArgs a;
+  const int rc = step_args(s, x, a);
+  if (rc != CRAFT_OK) return rc;
+  a.label = label_out;
+  // teacher lanes per env: 4 (default) or 1 (CRAFT_TEACH_LANES=1, diagnostic)
+  static const int tl = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 1) ? 1 : 4;
+  const int tile = craft::kMaxTileEnvs;
+  const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4;
+  hipError_t e = craft::launch_tick_teach(tl, (s->view.C + 31) / 32, s->cfg.window_width, s->view, a, lds,
+                                          reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
+  return CRAFT_OK;
+}
+
+int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
+  if (!s || !x) return CRAFT_EINVAL;
+  TileArgs a;
+  const int rc = step_args(s, x, a);
+  if (rc != CRAFT_OK) return rc;
   return launch(s, craft::MODE_TICK, a, stream, "craft_step launch");
 }
 
@@ -604,10 +634,16 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   a.chunk = s->rollout_chunk > 0 ? s->rollout_chunk : (n_ticks > 0 ? n_ticks : 1);
   a.queue = reinterpret_cast<unsigned long long*>(s->d_sync);
   a.tile_done = reinterpret_cast<uint32_t*>(s->d_sync + 16);
-  if (n_ticks > 0)
-    HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
   int tile = 0, threads = 0, split = 0;
   rollout_shape(s, &tile, &threads, &split);
+  // the work-unit queue and hand-off flags: every kernel shape but the split kernel's
+  // continuous pipeline (one unit per tile, observations on), which assigns tiles statically
+  // (CRAFT_UNIT_PIPELINE=1 in the environment: diagnostic, one pipeline per tile instead)
+  static const bool unit_pipeline = getenv("CRAFT_UNIT_PIPELINE") != nullptr;
+  const bool flat = split && a.chunk >= n_ticks && obs != nullptr && !unit_pipeline;
+  a.flat = flat ? 1 : 0;
+  if (n_ticks > 0 && !flat)
+    HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
   hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, s->view, a, lds_bytes(s, tile, 2, true),
                                        reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");

@@ -1,0 +1,45 @@
+// craft_tick_teach.hip — craft_step_teach: one rollout tick fused with the
+// DemonstrationTeacher on every env's new state (config 5: a DAgger label per
+// tick).  The tile kernel (craft_tile.h) with TILE * TL teacher threads beside
+// its 256: the tick's waves stream the observations while the teacher waves run
+// teach_env on the grid rows the tick left in LDS, so the teacher reads no grid
+// from HBM and needs no launch of its own.
+#include "craft_tile.h"
+
+namespace craft {
+
+template <int WIN, int TL, int NW>
+static hipError_t launch_tt(const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+  constexpr int TILE = kMaxTileEnvs;
+  const int64_t tiles = (a.n + TILE - 1) / TILE;
+  if (tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL((tile_kernel<WIN, MODE_TICK, TILE, TL, NW>), dim3((unsigned)tiles),
+                     dim3(kThreads + TILE * TL), lds, st, v, a);
+  return hipGetLastError();
+}
+
+template <int TL, int NW>
+static hipError_t launch_tt_win(int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+  switch (win) {
+    case 3: return launch_tt<3, TL, NW>(v, a, lds, st);
+    case 5: return launch_tt<5, TL, NW>(v, a, lds, st);
+    default: return launch_tt<7, TL, NW>(v, a, lds, st);
+  }
+}
+
+template <int TL>
+static hipError_t launch_tt_nw(int nw, int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+  // nw = 32-bit words per cell set: 8x8 -> 2, 10x10 -> 4, 12x12 -> 5, 16x16 -> 8
+  if (nw <= 2) return launch_tt_win<TL, 2>(win, v, a, lds, st);
+  if (nw <= 4) return launch_tt_win<TL, 4>(win, v, a, lds, st);
+  if (nw <= 5) return launch_tt_win<TL, 5>(win, v, a, lds, st);
+  return launch_tt_win<TL, 8>(win, v, a, lds, st);
+}
+
+// tl = teacher lanes per env: 4 (a quad per env, 4 teacher waves) or 1 (one wave).
+hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
+                             hipStream_t st) {
+  return tl == 1 ? launch_tt_nw<1>(nw, win, v, a, lds, st) : launch_tt_nw<4>(nw, win, v, a, lds, st);
+}
+
+}  // namespace craft

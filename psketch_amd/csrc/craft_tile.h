@@ -1,0 +1,308 @@
+// craft_tile.h — the hot kernel: one rollout tick (or transition / observe /
+// reset) for a tile of TILE consecutive envs per 256-thread workgroup.
+//
+//   A  wave 0, one lane per env: load the env's packed state word, inventory,
+//      cleared-cell mask, restart spec and action (one HBM round trip), then its
+//      scenario row from the L2-resident pool, straight into LDS; the static
+//      task / recipe tables come along.  No workgroup barrier.
+//   C  same lanes: run the rollout protocol and CraftState.step on the LDS grid,
+//      write the state back.  Meanwhile waves 1-3 zero the tile's observation
+//      bytes in LDS.
+//   D  all threads scatter the observation's non-zero bytes (local-window
+//      one-hots, block-max-pooled one-hots, inventory counts, dir one-hot) into
+//      the tile's u8 rows [TILE][F] in LDS.
+//   E  all threads stream the rows to HBM: flat index s, one LDS read, one
+//      contiguous 16-byte store (fp32: ds_read_b32 of 4 feature bytes and 4
+//      v_cvt_f32_ubyte; bf16: 8 bytes; u8: 16 bytes as they are).
+// The kernel is bound by E's HBM writes (F*4 = 1616 B per env at w=3).  See
+// DESIGN.md for the roofline and the phase timings that shaped this layout.
+#pragma once
+#include "craft_obs.h"
+#include "craft_teach.h"
+
+namespace craft {
+
+// TL > 0 (MODE_TICK only): TILE * TL more threads run the DemonstrationTeacher on
+// every env's new state (craft_step_teach), TL lanes per env, while the first
+// kThreads stream the observations: the BFS reads the grid rows the tick left in
+// LDS.  NW = 32-bit words per cell set (teach_env).
+template <int WIN, int MODE, int TILE, int TL = 0, int NW = 0>
+__global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, TileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
+  uint8_t* s_grid = smem;
+  uint8_t* s_obs = smem + lay.obs;
+  uint8_t* s_inv = smem + lay.inv;
+  uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
+  uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
+  uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
+  uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.bytes);   // TL > 0: [TILE] task | frozen << 8
+
+  const int tid = threadIdx.x;
+  const int64_t env0 = (int64_t)blockIdx.x * TILE;
+  const int nE = (int)min((int64_t)TILE, a.n - env0);
+  const bool want_obs = a.obs != nullptr;
+  const int F = v.F;
+
+  STAMP(0);
+  // ---- A + C: wave 0, one lane per env ------------------------------------------------------
+  if (tid < TILE) {
+    for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
+    for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += TILE) s_rc[t] = v.rcw[t];
+
+    int64_t slot = 0, dslot = 0;
+    bool live = tid < nE;
+    uint32_t init_word = 0;
+    int act = 0;
+    uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0, m0 = i0, m1 = i0;
+    Agent s{};
+    if (live) {
+      const int64_t i = env0 + tid;
+      slot = (MODE == MODE_TICK || MODE == MODE_RESET || !a.src) ? i : (int64_t)a.src[i];
+      dslot = (MODE == MODE_TRANSITION && a.dst) ? (int64_t)a.dst[i] : slot;
+      if (slot < 0 || slot >= v.n_envs || dslot < 0 || dslot >= v.n_envs) {
+        latch_error(v.err, CRAFT_ERANGE, i);
+        live = false;
+      }
+    }
+    if (live) {
+      if (MODE == MODE_RESET) {
+        const int64_t i = env0 + tid;
+        const int sc = a.r_scen[i], x0 = a.r_x[i], y0 = a.r_y[i], d0 = a.r_dir[i], tk = a.r_task[i];
+        if (sc < 0 || sc >= v.pool_count || x0 < 1 || x0 > v.W - 2 || y0 < 1 || y0 > v.H - 2 ||
+            d0 < 0 || d0 > 3 || tk < 0 || tk >= v.n_tasks) {
+          latch_error(v.err, CRAFT_EINVAL, i);
+          live = false;
+        } else {
+          s.x = x0; s.y = y0; s.dir = d0; s.frozen = 0; s.timer = v.maxT; s.scen = sc; s.task = tk;
+        }
+      } else {
+        const uint64_t st = v.state[slot];
+        if (MODE == MODE_TICK || MODE == MODE_TRANSITION) init_word = v.init[slot];
+        if (MODE == MODE_TICK) {
+          if (a.actions) {
+            act = a.actions[slot];
+          } else {
+            const uint64_t gid = (uint64_t)(v.env_base + slot);
+            act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)a.tick) >> 32) % 6u);
+          }
+          if (a.bc && a.bc[slot]) act = a.ref[slot];    // behaviour cloning, imitation.py:56-57
+        } else if (MODE == MODE_TRANSITION) {
+          act = a.actions[env0 + tid];
+        }
+        i0 = v.inv[2 * slot];
+        i1 = v.inv[2 * slot + 1];
+        m0 = v.mask[2 * slot];
+        m1 = v.mask[2 * slot + 1];
+        s = unpack_state(st);
+        if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
+          latch_error(v.err, CRAFT_EINVAL, slot);   // never initialised by reset / set_state
+          live = false;
+        }
+      }
+    }
+    uint8_t* g = s_grid + tid * v.GS;
+    if (live) {
+      // the env's scenario grid: CS/16 independent 16-byte loads (L2-resident pool)
+      const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(g);
+      const int nchunk = v.CS >> 4;
+      uint4 c[CRAFT_MAX_CELLS / 16];
+#pragma unroll
+      for (int q = 0; q < CRAFT_MAX_CELLS / 16; ++q)
+        if (q < nchunk) c[q] = src[q];
+#pragma unroll
+      for (int q = 0; q < CRAFT_MAX_CELLS / 16; ++q)
+        if (q < nchunk) {
+          dst[4 * q + 0] = c[q].x; dst[4 * q + 1] = c[q].y; dst[4 * q + 2] = c[q].z; dst[4 * q + 3] = c[q].w;
+        }
+    }
+    // Every LDS word written above is read below by the same lane, or (the
+    // tables) by lanes of this same wave: order the wave's LDS accesses.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP(1);
+
+    // ---- C ----
+    uint32_t* ivw = reinterpret_cast<uint32_t*>(s_inv + tid * kInvStride);
+    uint8_t* iv = s_inv + tid * kInvStride;
+    uint32_t m[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+    ivw[0] = i0.x; ivw[1] = i0.y; ivw[2] = i0.z; ivw[3] = i0.w;
+    ivw[4] = i1.x; ivw[5] = i1.y; ivw[6] = i1.z; ivw[7] = i1.w;
+    bool inv_changed = false, mask_changed = false;
+    int d = 0, succ = -1, counted = 0;
+    int code = -1;                                         // transition code (craft.h)
+    if (live) {
+      // The LDS row holds pool[scenario]; cells cleared this episode are applied
+      // lazily, so an auto-reset (which restores exactly that row) needs no reload.
+      bool restart = false;
+      if (MODE == MODE_TICK) {
+        // per-env body of ImitationTrainer.do_rollout, trainers/imitation.py:59-73
+        if (s.frozen) {
+          d = 1;
+        } else {
+          counted = 1;
+          s.timer -= 1;
+          d = (act == CRAFT_STOP) || s.timer <= 0;
+          restart = d && (a.flags & CRAFT_STEP_AUTORESET);
+        }
+        if (d) {
+          // satisfies() of the pre-step state: only the facing cell and the inventory matter
+          const uint32_t tt = s_task[s.task];
+          const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));
+          uint32_t mw = 0;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) mw |= (w == (fc >> 5)) ? m[w] : 0u;
+          const int goal = tt & 0xf, arg = (tt >> 4) & 0xff;
+          if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) succ = iv[arg] > 0;
+          else if (goal == CRAFT_GOAL_GO) succ = (((mw >> (fc & 31)) & 1u) ? 0 : (int)g[fc]) == arg;
+          else succ = -1;
+        }
+      }
+      if (!restart) {
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {                     // cells cleared this episode
+          uint32_t mm = m[w];
+          while (mm) {
+            g[w * 32 + __ffs(mm) - 1] = 0;
+            mm &= mm - 1;
+          }
+        }
+      }
+      if (MODE == MODE_RESET) {
+        inv_changed = mask_changed = true;
+      } else if (MODE == MODE_TICK) {
+        if (restart) {                                    // CraftScenario.init, craft.py:268-273
+          s.x = init_word & 0xff; s.y = (init_word >> 8) & 0xff; s.dir = (init_word >> 16) & 3;
+          s.timer = v.maxT;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) { ivw[w] = 0u; m[w] = 0u; }
+          inv_changed = mask_changed = true;
+        } else if (d && !s.frozen) {
+          s.frozen = 1;
+          s.timer = max(s.timer, 0);
+        } else if (!d) {
+          if (act < 0 || act >= CRAFT_N_ACTIONS) {
+            latch_error(v.err, CRAFT_EBADACTION, slot);
+          } else {
+            const int ox = s.x, oy = s.y;
+            transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+            code = transition_code(ox, oy, s, inv_changed);
+          }
+        }
+      } else if (MODE == MODE_TRANSITION) {
+        if (act >= CRAFT_N_ACTIONS) {
+          latch_error(v.err, CRAFT_EBADACTION, slot);
+        } else if (act >= 0) {
+          const int ox = s.x, oy = s.y;
+          transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+          code = transition_code(ox, oy, s, inv_changed);
+        }
+        if (dslot != slot) inv_changed = mask_changed = true;   // copy-on-step
+      } else if (MODE == MODE_OBSERVE) {
+        if (a.sat) {
+          const int tk = a.tasks ? a.tasks[env0 + tid] : s.task;
+          if (tk < 0 || tk >= v.n_tasks) {
+            latch_error(v.err, CRAFT_ERANGE, env0 + tid);
+            a.sat[env0 + tid] = -1;
+          } else {
+            a.sat[env0 + tid] = (int8_t)satisfies(v, g, iv, s, s_task[tk]);
+          }
+        }
+      }
+      // write back
+      if (MODE != MODE_OBSERVE) v.state[dslot] = pack_state(s);
+      if (MODE == MODE_RESET) v.init[dslot] = (uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16);
+      if (MODE == MODE_TRANSITION && dslot != slot) v.init[dslot] = init_word;
+      if (inv_changed) {
+        v.inv[2 * dslot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+        v.inv[2 * dslot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
+      }
+      if (mask_changed) {
+        v.mask[2 * dslot] = make_uint4(m[0], m[1], m[2], m[3]);
+        v.mask[2 * dslot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
+      }
+      if (MODE == MODE_TICK) {
+        const int64_t i = env0 + tid;
+        if (a.done) a.done[i] = (uint8_t)d;
+        if (a.sat) a.sat[i] = (int8_t)succ;
+        if (a.reward) a.reward[i] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+        if (a.rec) a.rec[i] = counted ? act : -1;        // action_seqs, imitation.py:59-61
+      }
+    }
+    if ((MODE == MODE_TICK || MODE == MODE_TRANSITION) && a.code && tid < nE) a.code[env0 + tid] = (int8_t)code;
+    s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
+    if (TL > 0) s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8);
+    if (MODE == MODE_TICK) {
+      // episode statistics: one partial-sum row per workgroup (uncontended)
+      const uint64_t bs = __ballot(live && counted && d && succ == 1);
+      const uint64_t be = __ballot(live && counted && d);
+      const uint64_t bt = __ballot(live && counted);
+      const uint64_t bl = __ballot(live && counted && !d);
+      if (tid == 0) {   // no-return atomics: the wave does not wait for them
+        unsigned long long* r = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
+        atomicAdd(r + 0, (unsigned long long)__popcll(bs));
+        atomicAdd(r + 1, (unsigned long long)__popcll(be));
+        atomicAdd(r + 2, (unsigned long long)__popcll(bt));
+        if (a.any_live && bl) *a.any_live = 1;          // idempotent plain store
+      }
+    }
+  } else if (want_obs && tid < kThreads) {
+    // waves 1-3: zero the tile's observation bytes while wave 0 runs A + C
+    uint4* z = reinterpret_cast<uint4*>(s_obs);
+    const int n16 = (nE * F + 15) >> 4;
+    for (int i = tid - TILE; i < n16; i += kThreads - TILE) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  STAMP(3);
+  if (TL == 0 && !want_obs) {
+    STAMP_END();
+    return;
+  }
+  __syncthreads();
+  STAMP(4);
+
+  // ---- D: scatter the observation's non-zero bytes ---------------------------------------------
+  if (want_obs && tid < kThreads) scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
+  if (want_obs) __syncthreads();
+  STAMP(5);
+
+  if (TL > 0 && tid >= kThreads) {
+    // ---- T: DemonstrationTeacher on the new state (teachers/demonstration.py:9-30) from the
+    // grid row the tick left in LDS (cleared cells already applied), overlapping E ----------
+    const int u = tid - kThreads, e = u / TL, ql = u % TL;
+    if (e < nE) {
+      const int64_t i = env0 + e;
+      const uint32_t ag = s_agent[e], ti = s_tinfo[e];
+      int action = -2;                                    // a slot C could not run (error latched)
+      if (ag && ((ti >> 8) & 1u)) {
+        action = -1;                                      // frozen: the trainer's label for a done env
+      } else if (ag) {
+        Agent s{};
+        s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
+        const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int len = -1, err = 0;
+        action = teach_env<NW, TL>(v, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS), m0,
+                                   s_inv + e * kInvStride, s, s.task, ql, false, len, err);
+        if (err && ql == 0) latch_error(v.err, err, i);
+      }
+      if (ql == 0) a.label[i] = action;
+    }
+    STAMP_END();
+    return;
+  }
+  if (!want_obs) {
+    STAMP_END();
+    return;
+  }
+
+  // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
+  switch (v.obs_fmt) {
+    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    default: stream_obs<CRAFT_OBS_F32>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+  }
+  STAMP_END();
+}
+
+}  // namespace craft

@@ -21,7 +21,10 @@ def world():
 
 
 def init(device=None, backend=None):
-    """Initialise the process group when WORLD_SIZE > 1 (RCCL for GPUs, gloo on CPU)."""
+    """Initialise the process group when WORLD_SIZE > 1 (RCCL for GPUs, gloo on
+    CPU; backend="gloo" with a GPU device keeps the data on the GPU and runs the
+    two scalar collectives through host copies — a rehearsal of several ranks on
+    one card)."""
     rank, ws, _ = world()
     if ws > 1 and not dist.is_initialized():
         if backend is None:
@@ -29,6 +32,17 @@ def init(device=None, backend=None):
         kw = {"device_id": device} if backend == "nccl" and device is not None else {}
         dist.init_process_group(backend, **kw)
     return rank, ws
+
+
+def _reduce(t, op):
+    """all_reduce in place; through a host copy when the backend is gloo and t is on a GPU."""
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
 
 
 def env_shard(rank, envs_per_rank):
@@ -43,14 +57,14 @@ def active():
 def reduce_episode_stats(stats):
     """Sum the int64[3] episode summaries of all ranks (in place)."""
     if active():
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
+        _reduce(stats, dist.ReduceOp.SUM)
     return stats
 
 
 def max_over_ranks(value, device):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     if active():
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _reduce(t, dist.ReduceOp.MAX)
     return float(t.item())
 
 

@@ -210,16 +210,19 @@ class CraftSim:
 
     def step(self, actions=None, seed=0, tick=0, autoreset=True, obs=None, reward=None, done=None,
              success=None, ref_actions=None, behavior_clone=None, action_record=None,
-             any_live=None, transition_code=None):
+             any_live=None, transition_code=None, labels=None):
         """One rollout tick for every slot (include/craft.h craft_step / craft_step_ex).
         actions: int32 device tensor [N] or None for the in-kernel hashed draw;
         ref_actions + behavior_clone (uint8 [N]): cloned actions; action_record
         (int32 [N]) receives the action taken (-1 for done slots); any_live (a
-        one-element int32 device tensor) is set to 1 if a slot is still running."""
+        one-element int32 device tensor) is set to 1 if a slot is still running.
+        labels (int32 [N]): the DemonstrationTeacher's action for every slot's NEW
+        state, computed in the same launch (craft_step_teach) — what teacher()
+        would return right after this step."""
         n = self.n_envs
         flags = N.STEP_AUTORESET if autoreset else 0
         if ref_actions is None and behavior_clone is None and action_record is None \
-                and any_live is None and transition_code is None:
+                and any_live is None and transition_code is None and labels is None:
             # plain tick: the short craft_step entry (least host overhead per launch)
             a = self._i32(actions, n) if actions is not None else None
             r = self._buf("reward", reward, torch.float32, (n,))
@@ -257,7 +260,13 @@ class CraftSim:
         args.action_seed = seed & (2**64 - 1)
         args.tick = int(tick)
         args.flags = flags
-        self._check(N.lib().craft_step_ex(self._h, ctypes.byref(args), self._stream()), "craft_step")
+        if labels is not None:
+            self._buf("labels", labels, torch.int32, (n,))
+            self._check(N.lib().craft_step_teach(self._h, ctypes.byref(args), _ptr(labels),
+                                                 self._stream()), "craft_step_teach")
+        else:
+            self._check(N.lib().craft_step_ex(self._h, ctypes.byref(args), self._stream()),
+                        "craft_step")
         return obs
 
     def rollout(self, n_ticks, seed=0, tick0=0, actions=None, autoreset=True, obs=None,

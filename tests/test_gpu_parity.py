@@ -494,37 +494,48 @@ def test_empty_and_single_env_calls(gpu):
     sim.check()
 
 
-def test_bench_rollout_equals_steps_at_full_size():
+@pytest.mark.parametrize("launches,R,chunk", [
+    ((32,), 16, 0),          # the bench's default launch
+    ((20, 13), 16, 0),       # the driver's --steps 20 launch, then a ragged one
+    ((32,), 32, 4),          # chunked units, ring >= launch: write-through state hand-off
+    ((24,), 8, 3)])          # chunked units, ring < launch: full release between units
+def test_bench_rollout_equals_steps_at_full_size(launches, R, chunk):
     """BASELINE's single-GPU size (65536 envs, 12x12 craft_medium, w=3), the
-    bench's own path: one 32-tick craft_rollout launch into a 16-slot ring with
-    the default workgroup shape, against 32 craft_step launches.  Every
+    bench's own path: craft_rollout launches into a ring with the default
+    workgroup shape, against one craft_step launch per tick.  Every
     observation, reward, done and success and the final states are identical
-    (compared on the device), and the episode counters agree."""
+    (compared on the device), and the episode counters agree.  The chunked
+    cases hand every tile between workgroups (possibly on other XCDs) several
+    times per launch, at full size."""
     world = "craft_medium_12x12"
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 1024)
-    n, K, R = 65536, 32, 16
+    n = 65536
     specs = synthetic_specs(pool, 12, 12, n, 0, seed=0, task_ids=[t.id for t in tm.dataset_tasks()])
     a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.tune_rollout(chunk, 0)
     a.reset(*specs)
     b.reset(*specs)
     F = a.n_features
     ring = torch.empty((R, n, F), dtype=torch.float32, device="cuda")
     outs = {k: torch.empty((R, n), dtype=dt, device="cuda") for k, dt in
             (("reward", torch.float32), ("done", torch.uint8), ("success", torch.int8))}
-    a.rollout(K, seed=5, tick0=0, obs=ring, **outs)
     obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
     one = {k: torch.empty(n, dtype=v.dtype, device="cuda") for k, v in outs.items()}
-    for t in range(K):
-        b.step(seed=5, tick=t, obs=obs, **one)
-        if t >= K - R:                           # the ring keeps the last R ticks
-            assert torch.equal(ring[t % R], obs), t
-            for k in outs:
-                assert torch.equal(outs[k][t % R], one[k]), (k, t)
-    sa, sb = a.get_state(), b.get_state()
-    for k in sa:
-        assert torch.equal(sa[k], sb[k]), k
+    t0 = 0
+    for K in launches:
+        a.rollout(K, seed=5, tick0=t0, obs=ring, **outs)
+        for t in range(t0, t0 + K):
+            b.step(seed=5, tick=t, obs=obs, **one)
+            if t >= t0 + K - R:                  # the ring keeps the launch's last R ticks
+                assert torch.equal(ring[t % R], obs), t
+                for k in outs:
+                    assert torch.equal(outs[k][t % R], one[k]), (k, t)
+        t0 += K
+        sa, sb = a.get_state(), b.get_state()
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), k
     np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
-    assert host(a.stats())[2] == n * K
+    assert host(a.stats())[2] == n * sum(launches)
     a.check()
     b.check()

@@ -1,0 +1,89 @@
+"""craft_step_teach (config 5's tick): one launch that steps every env and labels
+its new state with the DemonstrationTeacher (teachers/demonstration.py:9-30,
+teachers/base.py:10-87), checked against craft_step_ex followed by the
+standalone craft_teacher (itself pinned by the reference's 4400
+demonstrations) and, on a sample, against the per-target BFS oracle."""
+import numpy as np
+import pytest
+import torch
+
+from psketch_amd import sample_scenarios, synthetic_specs
+from tests.helpers import make_tables
+from tests.test_gpu_parity import host, sim_with_pool
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("world,W,n,T,autoreset,given", [
+    ("craft_medium_12x12", 12, 65536, 45, True, False),     # config 5's size, across episode ends
+    ("craft_medium_12x12", 12, 5000, 45, False, True),      # frozen envs (label -1), a partial tile
+    ("craft_medium", 8, 3000, 30, True, True),              # 8x8: two words per cell set
+    ("craft_medium_12x12_w5", 12, 2048, 20, True, False),
+    ("craft_large", 10, 1024, 20, True, False)])            # 10x10: four words per cell set
+def test_step_teach_equals_step_then_teacher(world, W, n, T, autoreset, given):
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 256)
+    specs = synthetic_specs(pool, W, W, n, 0, seed=6, task_ids=[t.id for t in tm.dataset_tasks()])
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.reset(*specs)
+    b.reset(*specs)
+    F = a.n_features
+    rng = np.random.RandomState(2)
+    oa, ob = (torch.empty((n, F), dtype=torch.float32, device="cuda") for _ in range(2))
+    da, db = (torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(2))
+    la = torch.empty(n, dtype=torch.int32, device="cuda")
+    for t in range(T):
+        acts = (torch.as_tensor(rng.randint(0, 6, size=n).astype(np.int32), device="cuda")
+                if given else None)
+        a.step(acts, seed=3, tick=t, autoreset=autoreset, obs=oa, done=da, labels=la)
+        b.step(acts, seed=3, tick=t, autoreset=autoreset, obs=ob, done=db)
+        lb, _ = b.teacher()
+        assert torch.equal(oa, ob), t
+        assert torch.equal(da, db), t
+        assert torch.equal(la, lb), t
+    if not autoreset:
+        assert bool((la == -1).any())                     # frozen envs are labelled -1
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
+    a.check()
+    b.check()
+
+
+def test_step_teach_vs_oracle(oracle_mod):
+    """The fused labels of 65536 mid-rollout envs against the literal BFS oracle
+    on 1024 of them."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 512)
+    n = 65536
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=8, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    sim.reset(*specs)
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    for t in range(9):
+        sim.step(seed=5, tick=t, labels=lab)
+    st = {k: host(v) for k, v in sim.get_state().items()}
+    sim.check()
+    lab = host(lab)
+    o = oracle_mod.Oracle(cfg, pool)
+    for i in np.random.RandomState(3).choice(n, 1024, replace=False):
+        x, y, d, _ = st["agent"][i]
+        env = o.env(st["grid"][i], x, y, d, st["inventory"][i])
+        rc, act = o.teacher(env, int(specs[4][i]))
+        assert rc == 0 and act == lab[i], i
+
+
+def test_step_teach_rejects_oversized_worlds():
+    """4*W*H > 1000 overflows the reference's fixed BFS queue (teachers/base.py:42):
+    refused before any launch, as craft_teacher does."""
+    from psketch_amd import _native as N
+    world = "craft_16x16_w7"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 8)
+    sim = sim_with_pool(world, 64, pool)
+    sim.reset(*synthetic_specs(pool, 16, 16, 64, 0, seed=0, task_ids=[t.id for t in tm.dataset_tasks()]))
+    lab = torch.empty(64, dtype=torch.int32, device="cuda")
+    with pytest.raises(N.CraftError):
+        sim.step(seed=0, tick=0, labels=lab)

@@ -37,6 +37,11 @@ def main():
     rec = torch.empty(n, dtype=torch.int32, device=dev)
     live = torch.zeros(1000, dtype=torch.int32, device=dev)
     W = torch.randn(sim.n_features, 6, device=dev).to(torch.bfloat16)
+    R = 16
+    ring = torch.empty((R, n, sim.n_features), dtype=torch.float32, device=dev)
+    rr = torch.empty((R, n), dtype=torch.float32, device=dev)
+    rd = torch.empty((R, n), dtype=torch.uint8, device=dev)
+    rs = torch.empty((R, n), dtype=torch.int8, device=dev)
     rows = {
         "step plain": lambda i: sim.step(seed=0, tick=i, obs=obs),
         "step fused": lambda i: sim.step(acts, tick=i, obs=obs, ref_actions=ref, behavior_clone=bc,
@@ -46,6 +51,7 @@ def main():
         "step +bc": lambda i: sim.step(acts, tick=i, obs=obs, ref_actions=ref, behavior_clone=bc,
                                        action_record=rec),
         "teacher": lambda i: sim.teacher(action_out=ref),
+        "rollout K=1": lambda i: sim.rollout(1, tick0=i, obs=ring, reward=rr, done=rd, success=rs),
         "policy": lambda i: (obs.to(torch.bfloat16) @ W).argmax(dim=1).to(torch.int32),
         "scalar read": lambda i: int(live[i]),
     }
