@@ -93,7 +93,8 @@ def parse(argv=None):
     p.add_argument("--rollout-threads", type=int, default=0,
                    help="craft_rollout threads per tile workgroup (0 = the library's default shape)")
     p.add_argument("--rollout-chunk", type=int, default=0,
-                   help="craft_rollout ticks per dynamically scheduled work unit (0 = the whole launch)")
+                   help="craft_rollout ticks per dynamically scheduled work unit (0 = the whole "
+                        "launch; -1 = one continuous pipeline per workgroup)")
     p.add_argument("--obs-only", action="store_true",
                    help="diagnostic: skip the reward/done/success rings (not a bench line)")
     p.add_argument("--seed", type=int, default=0)
@@ -325,7 +326,8 @@ def run(args):
             kname = (f"rollout_split_kernel<{win}, {tile}, {threads}, {fmt}, *, false>" if split
                      else f"rollout_kernel<{win}, {tile}, {threads}, {fmt}, *, false>")
             shape = {"tile": tile, "rollout_threads": threads, "split_producer": split,
-                     "rollout_chunk": args.rollout_chunk or k_eff}
+                     "rollout_unit_ticks": (k_eff if args.rollout_chunk <= 0 else args.rollout_chunk),
+                     "rollout_pipeline": "continuous" if args.rollout_chunk == -1 else "per unit"}
         else:
             tile, _ = sim.tile_shape()
             kname = f"tile_kernel<{win}, MODE_TICK, {tile}>"

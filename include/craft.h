@@ -154,7 +154,10 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * state passing between workgroups at chunk boundaries, so slow workgroups do
  * fewer units.  0 (default) = one unit per tile for the whole launch, which
  * measured fastest at 65536 envs (the balance gained does not pay for the
- * hand-offs).  threads: threads per tile workgroup on the tile
+ * hand-offs).  -1 = one continuous pipeline per workgroup across
+ * the tiles it claims (no pipeline fill and drain per tile, the next tile
+ * prefetched by LDS-DMA; the split kernel's 3x3 default shape only): measured
+ * level with 0.  threads: threads per tile workgroup on the tile
  * set by craft_sim_tune.  128 or 256: one producer wave, the rest stream; 64-env
  * tiles also take 512.  16- and 32-env tiles with 320, 384 or 512: the
  * split-producer kernel (transition and scatter on two waves, the other 3-6

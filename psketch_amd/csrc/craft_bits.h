@@ -96,20 +96,24 @@ __device__ __forceinline__ Bits<NW> bshift(const Bits<NW>& a, int d) {
   }
   return r;
 }
-// bshift for a shift amount known only at run time (the alignbit amount is a VGPR).
+// bshift for a shift amount known only at run time, which may differ between the
+// lanes of a wave (the quad-parallel teacher): branch-free, so lanes shifting up and
+// lanes shifting down do not diverge.  Word i of the result is the funnel shift of the
+// pair (sel[i+1], sel[i]), sel[j] = a[j-1] for an upward shift (amount 32 - d) and a[j]
+// for a downward one (amount -d).
 template <int NW>
 __device__ __forceinline__ Bits<NW> bshift_var(const Bits<NW>& a, int d) {
-  Bits<NW> r;
-  if (d > 0) {
-    r.w[0] = a.w[0] << d;
+  const bool up = d > 0;
+  const uint32_t t = up ? (uint32_t)(32 - d) : (uint32_t)(-d);
+  uint32_t sel[NW + 1];
 #pragma unroll
-    for (int i = 1; i < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i], a.w[i - 1], 32 - d);
-  } else {
-    const int s = -d;
-#pragma unroll
-    for (int i = 0; i + 1 < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i + 1], a.w[i], s);
-    r.w[NW - 1] = a.w[NW - 1] >> s;
+  for (int j = 0; j <= NW; ++j) {
+    const uint32_t lo = j >= 1 ? a.w[j - 1] : 0u, hi = j < NW ? a.w[j] : 0u;
+    sel[j] = up ? lo : hi;
   }
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(sel[i + 1], sel[i], t);
   return r;
 }
 

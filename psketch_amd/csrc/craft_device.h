@@ -139,7 +139,9 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   uint8_t* done;
   int8_t* sat;
   int32_t chunk;           // ticks per work unit
-  unsigned long long* queue;   // work-unit counter, zeroed before the launch
+  unsigned long long* queue;   // work-unit counter: unit = the value fetched - qbase
+  unsigned long long qbase;    // the counter's value at the launch (kept by the host)
+  int64_t* grid_out;       // host side only: the launch reports its grid size here
   uint32_t* tile_done;     // per tile: chunks completed in this launch, zeroed before the launch
   int32_t flat;            // split kernel, one unit per tile: one continuous pipeline (no queue)
 };
@@ -185,6 +187,17 @@ __device__ __forceinline__ void latch_error(int32_t* err, int code, int64_t slot
     err[2] = (int32_t)(slot & 0xffffffff);
     err[3] = (int32_t)(slot >> 32);
   }
+}
+
+// SWAR byte tests on a 32-bit word of 4 kind-id cells: bit 7 of each byte set where that
+// byte is nonzero / zero ((b & 0x7f) + 0x7f carries into bit 7 for any nonzero low bits).
+__device__ __forceinline__ uint32_t nonzero_bytes(uint32_t w) {
+  return (((w & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t w) { return ~nonzero_bytes(w) & 0x80808080u; }
+// The top bits of the 4 bytes of m (bits 7, 15, 23, 31) as a nibble.
+__device__ __forceinline__ uint32_t byte_tops(uint32_t m) {
+  return ((m >> 7) | (m >> 14) | (m >> 21) | (m >> 28)) & 0xfu;
 }
 
 __device__ __forceinline__ int kind_class(const SimView& v, int k) {

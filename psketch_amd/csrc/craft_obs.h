@@ -191,10 +191,19 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
         uint32_t w[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) w[q] = ivw[q];
-        uint8_t* irow = row + 2 * L;
+        uint8_t* irow = row + 2 * L;                                  // the row is zeroed: only the
+        uint32_t nz = 0;                                              // nonzero counts are written
 #pragma unroll
-        for (int k = 0; k < CRAFT_MAX_KINDS; ++k)
-          if (k < K) irow[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        for (int q = 0; q < 8; ++q) nz |= byte_tops(nonzero_bytes(w[q])) << (4 * q);
+        nz &= K >= 32 ? ~0u : ((1u << K) - 1u);
+        while (nz) {
+          const int k = __ffs(nz) - 1;
+          uint32_t wk = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) wk = (q == (k >> 2)) ? w[q] : wk;
+          irow[k] = (uint8_t)(wk >> (8 * (k & 3)));
+          nz &= nz - 1;
+        }
       }
       row[2 * L + K + dir] = 1;                                     // dir one-hot
     } else {

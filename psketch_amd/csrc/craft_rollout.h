@@ -243,7 +243,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
 
   for (;;) {
     // ---- next unit ------------------------------------------------------------------------------
-    if (tid == 0) s_ctrl[0] = (uint32_t)atomicAdd(a.queue, 1ull);
+    if (tid == 0) s_ctrl[0] = (uint32_t)(atomicAdd(a.queue, 1ull) - a.qbase);
     __syncthreads();
     const uint32_t u = s_ctrl[0];
     if (u >= n_units) break;                            // workgroup-uniform exit
@@ -483,6 +483,7 @@ static hipError_t launch_rollout_one(const SimView& v, const RolloutArgs& a, siz
   // every workgroup owns one stats_part row; the handle has (n_envs + 15) / 16 of them
   const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;
   const int64_t grid = std::min<int64_t>((units + rounds - 1) / rounds, rows);
+  if (a.grid_out) *a.grid_out = grid;
   hipLaunchKernelGGL((rollout_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>), dim3((unsigned)grid), dim3(NT), lds, st, v, a);
   return hipGetLastError();
 }
@@ -494,8 +495,11 @@ static hipError_t launch_rollout_split_one(const SimView& v, const RolloutArgs& 
   const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
   if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
   constexpr int WPE = WIN == 3 ? CRAFT_SPLIT_WPE : 2;
-  const size_t lds = (size_t)split_lds_bytes(TILE, v.GS, v.F);
-  auto kern = rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>;
+  const size_t lds = (size_t)split_lds_bytes(TILE, v.GS, v.F, v.CS);
+  // the continuous-pipeline instantiation exists for the default 3x3 shape only
+  constexpr bool kFlatShape = WIN == 3 && TILE == 32 && NT == 512;
+  auto kern = (kFlatShape && a.flat) ? rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, kFlatShape>
+                                     : rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>;
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -515,6 +519,7 @@ static hipError_t launch_rollout_split_one(const SimView& v, const RolloutArgs& 
   const int64_t rounds = (units + resident - 1) / resident;
   const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;
   const int64_t grid = std::min<int64_t>((units + rounds - 1) / rounds, rows);
+  if (a.grid_out) *a.grid_out = grid;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, st, v, a);
   return hipGetLastError();
 }

@@ -31,20 +31,30 @@
 // in craft_rollout.h, and the results are identical (the same tests run both
 // kernels).
 #pragma once
+#include <type_traits>
+
 #include "craft_obs.h"
 
 namespace craft {
 
 // LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation
 // rows [2][up16(TILE*F)] | inventory rows [2][TILE][36] | agent words [2][TILE] |
-// task table [64] u16 | recipe words [16][3] | control words [4] | item words [4][2].
-__host__ __device__ inline int split_lds_bytes(int tile, int GS, int F) {
+// task table [64] u16 | recipe words [16][3] | control words [4] | item words [4][2] |
+// output words [4][TILE] | next-tile staging: state [TILE] u64, init [TILE] u32,
+// inventory and mask [TILE][32 B] each, pool rows [TILE][CS].
+// (+ the publish outbox: state [TILE] u64, mask [TILE][8] u32)
+__host__ __device__ inline int split_stage_bytes(int tile, int CS) { return tile * (8 + 4 + 64) + tile * CS + tile * 40; }
+__host__ __device__ inline int split_lds_bytes(int tile, int GS, int F, int CS) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   return up16(3 * tile * GS) + 2 * up16(tile * F) + 2 * tile * kInvStride + 2 * tile * 4 +
-         CRAFT_MAX_TASKS * 2 + CRAFT_MAX_RECIPES * 12 + 16 + 32;
+         CRAFT_MAX_TASKS * 2 + CRAFT_MAX_RECIPES * 12 + 16 + 32 + 4 * tile * 4 +
+         split_stage_bytes(tile, CS);
 }
 
-template <int WIN, int TILE, int NT, int FMT, int WPE, bool GIVEN>
+// FLAT: the continuous pipeline (one unit per tile, observations on: RolloutArgs.flat);
+// otherwise work units from the queue.  Separate instantiations, so that neither path's
+// registers count against the other.
+template <int WIN, int TILE, int NT, int FMT, int WPE, bool GIVEN, bool FLAT = false>
 __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(NT >= 192 && TILE <= 64, "a producer, a scatter wave and at least one streaming wave");
@@ -61,6 +71,11 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(s_task + CRAFT_MAX_TASKS);
   uint32_t* s_ctrl = s_rc + CRAFT_MAX_RECIPES * 3;
   uint32_t* s_item = s_ctrl + 4;                          // [4][2]: item j -> {tile + 1 (0 = none), tick}
+  // [4][TILE] by item & 3: done | success << 8 | reward << 16 | 1 << 24.  Four, not two: the
+  // streaming waves store item j's outputs two intervals after C wrote them, while C writes
+  // item j + 2's
+  uint32_t* s_out = s_item + 8;
+  uint8_t* s_stage = reinterpret_cast<uint8_t*>(s_out + 4 * TILE);   // 16-byte aligned (TILE % 4 == 0)
 
   const int tid = threadIdx.x;
   const int64_t n = v.n_envs;
@@ -110,8 +125,8 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     }
   };
 
-  // ---- C: tick k on buffer p (trainers/imitation.py:59-73) -------------------------------------
-  auto tick_c = [&](int k, int p) __attribute__((always_inline)) {
+  // ---- C: tick k on buffer p & 1 (trainers/imitation.py:59-73); p = the item index --------------
+  auto tick_c = [&](int k, int p, bool lds_out) __attribute__((always_inline)) {
     const int64_t tick = a.tick0 + k;
     const int64_t r = tick % a.ring;
     int d = 0, succ = -1, counted = 0;
@@ -197,10 +212,17 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
         }
       }
       st = pack_state(s);
-      const int64_t o = r * n + slot;
-      if (a.done) a.done[o] = (uint8_t)d;
-      if (a.sat) a.sat[o] = (int8_t)succ;
-      if (a.reward) a.reward[o] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+      if (lds_out) {                                    // stored by the streaming waves with E
+        s_out[(p & 3) * TILE + tid] = (uint32_t)(uint8_t)d | ((uint32_t)(uint8_t)(int8_t)succ << 8) |
+                                      ((uint32_t)(counted && d && succ == 1) << 16) | (1u << 24);
+      } else {
+        const int64_t o = r * n + slot;
+        if (a.done) a.done[o] = (uint8_t)d;
+        if (a.sat) a.sat[o] = (int8_t)succ;
+        if (a.reward) a.reward[o] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+      }
+    } else if (lds_out && tid < TILE) {
+      s_out[(p & 3) * TILE + tid] = 0u;
     }
     const uint64_t bs = __ballot(live && counted && d && succ == 1);
     const uint64_t be = __ballot(live && counted && d);
@@ -213,7 +235,20 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   };
 
   // ---- A: lanes < TILE of wave 0 take over tile t into buffer p (state, pool row, clears) -----
-  auto load_tile = [&](int t, int p) __attribute__((always_inline)) {
+  // next-tile staging (flat pipeline): state, init, inventory, mask, pool rows, filled by LDS-DMA
+  uint64_t* sg_state = reinterpret_cast<uint64_t*>(s_stage);
+  uint32_t* sg_init = reinterpret_cast<uint32_t*>(s_stage + TILE * 8);
+  uint4* sg_inv = reinterpret_cast<uint4*>(s_stage + TILE * 12);
+  uint4* sg_mask = reinterpret_cast<uint4*>(s_stage + TILE * 44);
+  uint8_t* sg_pool = s_stage + TILE * 76;
+  uint64_t* ob_state = reinterpret_cast<uint64_t*>(sg_pool + TILE * v.CS);   // publish outbox
+  uint32_t* ob_mask = reinterpret_cast<uint32_t*>(ob_state + TILE);
+
+  // STAGED (std::true_type / std::false_type): read the tile from the staging area (LDS) or
+  // from HBM -- two instantiations, so the compiler emits ds_read or global_load, never a
+  // flat load through a selected pointer
+  auto load_tile = [&](int t, int p, auto STAGED) __attribute__((always_inline)) {
+    constexpr bool staged = decltype(STAGED)::value;
     const int64_t env0 = (int64_t)t * TILE;
     const int nE = (int)min((int64_t)TILE, n - env0);
     slot = env0 + tid;
@@ -221,10 +256,18 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t ivr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (live) {
-      st = v.state[slot];
-      init_word = v.init[slot];
-      const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
-      const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+      uint4 i0, i1, m0, m1;
+      if constexpr (staged) {
+        st = sg_state[tid];
+        init_word = sg_init[tid];
+        i0 = sg_inv[2 * tid]; i1 = sg_inv[2 * tid + 1];
+        m0 = sg_mask[2 * tid]; m1 = sg_mask[2 * tid + 1];
+      } else {
+        st = v.state[slot];
+        init_word = v.init[slot];
+        i0 = v.inv[2 * slot]; i1 = v.inv[2 * slot + 1];
+        m0 = v.mask[2 * slot]; m1 = v.mask[2 * slot + 1];
+      }
       ivr[0] = i0.x; ivr[1] = i0.y; ivr[2] = i0.z; ivr[3] = i0.w;
       ivr[4] = i1.x; ivr[5] = i1.y; ivr[6] = i1.z; ivr[7] = i1.w;
       m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
@@ -244,22 +287,34 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
       // pool[scenario] -> the pristine row and grid buffer p; inventory -> buffer p
       uint32_t* g0 = reinterpret_cast<uint32_t*>(grid_of(p));
       uint32_t* pwm = reinterpret_cast<uint32_t*>(s_pristine + tid * GS);
-      const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
+      const uint4* gsrc = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
+      const uint4* lsrc = reinterpret_cast<const uint4*>(sg_pool + tid * v.CS);
       const int nchunk = v.CS >> 4;
-      for (int q0 = 0; q0 < nchunk; q0 += 4) {
-        uint4 cq[4];
+      if constexpr (staged) {                           // LDS -> LDS, one 16-byte chunk at a time
+        for (int q0 = 0; q0 < nchunk; ++q0) {
+          const uint4 c = lsrc[q0];
+          const int q = 4 * q0;
+          pwm[q + 0] = g0[q + 0] = c.x;
+          pwm[q + 1] = g0[q + 1] = c.y;
+          pwm[q + 2] = g0[q + 2] = c.z;
+          pwm[q + 3] = g0[q + 3] = c.w;
+        }
+      } else {                                          // HBM / L2: four chunks in flight
+        for (int q0 = 0; q0 < nchunk; q0 += 4) {
+          uint4 cq[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (q0 + j < nchunk) cq[j] = src[q0 + j];
+          for (int j = 0; j < 4; ++j)
+            if (q0 + j < nchunk) cq[j] = gsrc[q0 + j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (q0 + j < nchunk) {
-            const int q = 4 * (q0 + j);
-            pwm[q + 0] = g0[q + 0] = cq[j].x;
-            pwm[q + 1] = g0[q + 1] = cq[j].y;
-            pwm[q + 2] = g0[q + 2] = cq[j].z;
-            pwm[q + 3] = g0[q + 3] = cq[j].w;
-          }
+          for (int j = 0; j < 4; ++j)
+            if (q0 + j < nchunk) {
+              const int q = 4 * (q0 + j);
+              pwm[q + 0] = g0[q + 0] = cq[j].x;
+              pwm[q + 1] = g0[q + 1] = cq[j].y;
+              pwm[q + 2] = g0[q + 2] = cq[j].z;
+              pwm[q + 3] = g0[q + 3] = cq[j].w;
+            }
+        }
       }
       uint32_t* iv0 = reinterpret_cast<uint32_t*>(inv_of(p));
 #pragma unroll
@@ -285,19 +340,21 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
 
   // ---- the tile's state back to HBM from buffer p (its last item); the mask is rebuilt from
   // the rows: cells are only ever cleared, so mask = {c : pristine[c] != 0 and grid[c] == 0} ---
-  auto publish = [&](int p, bool sc1) __attribute__((always_inline)) {
+  // cleared = pristine byte nonzero and current byte zero, 4 cells per word (SWAR); fully
+  // unrolled so every mask word index is static
+  auto cleared_mask = [&](int p, uint32_t (&m)[8]) __attribute__((always_inline)) {
     const uint32_t* gw = reinterpret_cast<const uint32_t*>(grid_of(p));
-    const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of(p));
-    uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int q = 0; q < (v.CS >> 2); ++q) {
-      const uint32_t pp = pw[q], cc = gw[q];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const bool cleared = ((pp >> (8 * b)) & 0xffu) != 0 && ((cc >> (8 * b)) & 0xffu) == 0;
-        const int cell = 4 * q + b;
-        if (cleared) m[cell >> 5] |= 1u << (cell & 31);
-      }
-    }
+    for (int i = 0; i < 8; ++i) m[i] = 0u;
+#pragma unroll
+    for (int q = 0; q < CRAFT_MAX_CELLS / 4; ++q)
+      if (q < (v.C + 3) >> 2)
+        m[q >> 3] |= byte_tops(nonzero_bytes(pw[q]) & zero_bytes(gw[q])) << (4 * (q & 7));
+  };
+  auto publish = [&](int p, bool sc1) __attribute__((always_inline)) {
+    const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of(p));
+    uint32_t m[8];
+    cleared_mask(p, m);
     if (sc1) {
       // write-through (sc1) stores: the hand-off form of MI355X_MICROARCH.md "Valid forms"
       // ({sc1 stores} -> every storing wave's s_waitcnt vmcnt(0) -> one lane's flag)
@@ -335,10 +392,19 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   };
 
   // ---- E on waves 2..: stream tick k of tile t from buffer p to its ring slot ------------------
-  auto stream_e = [&](int p, int t, int k) __attribute__((always_inline)) {
+  auto stream_e = [&](int p, int t, int k, bool outs) __attribute__((always_inline)) {
     const int64_t env0 = (int64_t)t * TILE;
     const int nE = (int)min((int64_t)TILE, n - env0);
     const int64_t r = (a.tick0 + k) % a.ring;
+    if (outs && tid - 128 < nE) {                       // the tick's done / success / reward (flat pipeline)
+      const uint32_t w = s_out[(p & 3) * TILE + tid - 128];
+      if (w >> 24) {
+        const int64_t o = r * n + env0 + (tid - 128);
+        if (a.done) a.done[o] = (uint8_t)(w & 0xffu);
+        if (a.sat) a.sat[o] = (int8_t)((w >> 8) & 0xffu);
+        if (a.reward) a.reward[o] = ((w >> 16) & 1u) ? 1.0f : 0.0f;
+      }
+    }
     void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * esz;
 #ifndef CRAFT_ABL_NOE
     stream_obs<FMT, NT - 128, true>(s_obs + (p & 1) * obs_buf, out, env0, F, nE, v.obs_policy, tid - 128);
@@ -356,70 +422,205 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     for (int i = tid; i < (2 * obs_buf >> 4); i += NT) z[i] = make_uint4(0, 0, 0, 0);
   }
 
-  if (a.flat && n_chunks == 1 && want_obs) {
+  if constexpr (FLAT) {
     // ---- continuous pipeline: tiles b, b + G, ... of this workgroup, all ticks each ----------
 #ifdef CRAFT_STAMPS
-    // diagnostic build only: per-role totals in s_memrealtime ticks (10 ns) -> stamps[block][8]:
+    // diagnostic build only: per-role totals in s_memrealtime ticks (10 ns) -> stamps[block][16]:
     // 0 start, 1 wave 0 in produce, 2 wave 0 at the barrier, 3 wave 1 in D, 4 wave 1 at the
-    // barrier, 5 wave 2 in E, 6 end, 7 wave 0 in tile switches (publish + load)
-    unsigned long long t_beg = __builtin_amdgcn_s_memrealtime(), acc_work = 0, acc_wait = 0, acc_sw = 0;
+    // barrier, 5 wave 2 in E, 6 end, 7 wave 0 in tile switches, of which 8 the prefetch wait,
+    // 9 publish, 10 load; 11 issuing the prefetch
+    unsigned long long t_beg = __builtin_amdgcn_s_memrealtime();
 #define SPLIT_NOW() __builtin_amdgcn_s_memrealtime()
 #else
 #define SPLIT_NOW() 0ull
-    unsigned long long acc_work = 0, acc_wait = 0, acc_sw = 0;
 #endif
-    // wave-uniform state of wave 0: the tile in progress and its next tick
-    int cur_t = -1, cur_k = 0, next_j = 0;
+    unsigned long long acc_work = 0, acc_wait = 0, acc_sw = 0, acc_pub = 0, acc_vm = 0, acc_ld = 0, acc_dma = 0;
+    // wave-uniform state of wave 0: the tile in progress (-1 none yet, -2 none left), its next tick
+    int cur_t = -1, cur_k = 0;
+    // The next tile's state and pool rows are fetched ahead by LDS-DMA into a staging area
+    // (wave 0 issues no other global loads or per-tick stores, so its vmcnt counts only these
+    // and its tile claims), and a tile switch reads LDS instead of waiting out an HBM round
+    // trip behind the write stream (a load waits behind the stores already queued in the CU's
+    // memory pipeline).  Partial tiles load directly.
+    bool staged = false;                                // the staging area holds the next tile
+    auto stage_state = [&](int t2) __attribute__((always_inline)) {
+      const int64_t e0 = (int64_t)t2 * TILE;
+      const int l = tid;                                // 64 lanes, 16 bytes each
+      typedef __attribute__((address_space(1))) void* gp;
+      typedef __attribute__((address_space(3))) void* lp;
+      if (l < TILE / 2) __builtin_amdgcn_global_load_lds((gp)(v.state + e0 + 2 * l), (lp)sg_state, 16, 0, 0);
+      if (l < TILE / 4) __builtin_amdgcn_global_load_lds((gp)(v.init + e0 + 4 * l), (lp)sg_init, 16, 0, 0);
+#pragma unroll
+      for (int h = 0; h < 2 * TILE; h += 64) {
+        __builtin_amdgcn_global_load_lds((gp)(v.inv + 2 * e0 + h + l), (lp)(sg_inv + h), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gp)(v.mask + 2 * e0 + h + l), (lp)(sg_mask + h), 16, 0, 0);
+      }
+    };
+    auto stage_pool = [&]() __attribute__((always_inline)) {
+      typedef __attribute__((address_space(1))) void* gp;
+      typedef __attribute__((address_space(3))) void* lp;
+      const int per = v.CS >> 4;                        // 16-byte chunks per pool row
+      int e = tid / per, c = tid - (tid / per) * per;   // chunk f = f0 + tid is (e, c)
+      const int de = 64 / per, dc = 64 - (64 / per) * per;
+      for (int f0 = 0; f0 < TILE * per; f0 += 64) {
+        const int f = f0 + tid;
+        if (f < TILE * per) {
+          const int scen = (int)((sg_state[e] >> 32) & 0xffffffu) % max(1, v.pool_count);
+          __builtin_amdgcn_global_load_lds((gp)(v.pool + (size_t)scen * v.CS + 16 * c), (lp)(sg_pool + 16 * f0),
+                                           16, 0, 0);
+        }
+        e += de;                                        // advance (e, c) by 64 chunks
+        c += dc;
+        if (c >= per) { c -= per; ++e; }
+      }
+    };
+    // Tiles come from the queue counter (a.queue - a.qbase = tiles handed out in this launch),
+    // so a workgroup that runs slow takes fewer.  The next tile is claimed late, kF = 6 ticks
+    // before the switch (claiming it earlier would hand the launch's last tiles to whichever
+    // workgroups asked first, not to those that free up first); its id is read two ticks
+    // later (an atomic's return waits behind the CU's queued stores), its state words are
+    // fetched then, its pool rows one tick after that.  Every workgroup
+    // makes exactly one fetch past the last tile, so a launch advances the counter by
+    // n_tiles + gridDim.x and the host keeps qbase without re-zeroing the counter.
+    auto fetch_now = [&]() __attribute__((always_inline)) -> int {
+      unsigned long long r = 0;
+      if (tid == 0) r = atomicAdd(a.queue, 1ull);
+      const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r) - (uint32_t)a.qbase;
+      return d < (uint32_t)n_tiles ? (int)d : -1;       // (a launch hands out < 2^32 units: low words)
+    };
+    const int K = a.n_ticks;
+    const int kF = max(0, K - 6), kA = max(0, K - 4), kB = max(0, K - 3);
+    uint32_t pend = 0;                                  // lane 0: the claim in flight
+    int64_t pub_slot = -1;                              // per lane: a finished env whose state is in the outbox
+    int t_next = -1;
     auto produce = [&](int j) __attribute__((always_inline)) {                         // wave 0: item j into buffer j & 1
-      if (cur_t != -2 && (cur_t < 0 || cur_k == a.n_ticks)) {
+      if (cur_t != -2 && (cur_t < 0 || cur_k == K)) {
         const unsigned long long s0 = SPLIT_NOW();
-        if (cur_t >= 0 && tid < TILE && live) publish((j - 1) & 1, false);
-        const int t = (int)blockIdx.x + next_j * (int)gridDim.x;
-        ++next_j;
-        if (t < n_tiles) {
+        const int t = cur_t == -1 ? fetch_now() : t_next;
+        if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the pool rows have landed
+        const unsigned long long s1 = SPLIT_NOW();
+        // the finished tile's state goes out AFTER the next one is loaded (its mask, which needs
+        // the pristine rows load_tile replaces, waits in an LDS outbox), so that no wait in
+        // load_tile also waits out these stores
+        const bool pub = cur_t >= 0 && tid < TILE && live;
+        const int64_t pslot = slot;
+        if (pub) {
+          uint32_t m[8];
+          cleared_mask((j - 1) & 1, m);
+          ob_state[tid] = st;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ob_mask[8 * tid + i] = m[i];
+        }
+        const unsigned long long s2 = SPLIT_NOW();
+        if (t >= 0) {
           cur_t = t;
           cur_k = 0;
-          if (tid < TILE) load_tile(t, j & 1);
+          if (tid < TILE) {
+            if (staged) load_tile(t, j & 1, std::true_type{});
+            else load_tile(t, j & 1, std::false_type{});
+          }
         } else {
           cur_t = -2;                                   // no tile left: the pipeline drains
         }
-        acc_sw += SPLIT_NOW() - s0;
+        staged = false;
+        t_next = -1;
+        pub_slot = pub ? pslot : -1;
+        const unsigned long long s3 = SPLIT_NOW();
+        acc_sw += s3 - s0;
+        acc_vm += s1 - s0;
+        acc_pub += s2 - s1;
+        acc_ld += s3 - s2;
       }
       const bool have = cur_t >= 0;
-      if (have && tid < TILE) tick_c(cur_k, j & 1);
+      if (have) {
+        const unsigned long long d0 = SPLIT_NOW();
+        if (cur_k == kF && tid == 0) pend = (uint32_t)atomicAdd(a.queue, 1ull);   // claim the next tile
+        if (cur_k == kA) {
+          const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend) - (uint32_t)a.qbase;
+          t_next = d < (uint32_t)n_tiles ? (int)d : -1;
+          if (t_next >= 0 && (int64_t)(t_next + 1) * TILE <= n) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // earlier staging reads are done
+            stage_state(t_next);
+          }
+        }
+        if (cur_k == kB && t_next >= 0 && (int64_t)(t_next + 1) * TILE <= n) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the state words have landed
+          stage_pool();
+          staged = true;
+        }
+        acc_dma += SPLIT_NOW() - d0;
+      }
+      if (have && tid < TILE) tick_c(cur_k, j, true);
+      if (pub_slot >= 0) {                              // the finished tile's state, last: nothing waits on it
+        const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of((j - 1) & 1));
+        const uint32_t* mw = ob_mask + 8 * tid;
+        v.state[pub_slot] = ob_state[tid];
+        v.inv[2 * pub_slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+        v.inv[2 * pub_slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
+        v.mask[2 * pub_slot] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
+        v.mask[2 * pub_slot + 1] = make_uint4(mw[4], mw[5], mw[6], mw[7]);
+        pub_slot = -1;
+      }
       if (tid == 0) {
         s_item[2 * (j & 3)] = have ? (uint32_t)cur_t + 1u : 0u;
         s_item[2 * (j & 3) + 1] = (uint32_t)cur_k;
       }
       if (have) ++cur_k;
     };
-    if (tid < 64) produce(0);
-    __syncthreads();
-    for (int i = 0;; ++i) {                             // interval i: C(i+1) | D(i) | E(i-1)
-      const unsigned long long w0 = SPLIT_NOW();
-      if (tid < 64) {
-        produce(i + 1);
-      } else if (tid < 128) {
-        const uint32_t t1 = s_item[2 * (i & 3)];
-        if (t1) scatter_d(i & 1, (int)min((int64_t)TILE, n - (int64_t)(t1 - 1) * TILE));
-      } else if (i >= 1) {
-        const uint32_t t1 = s_item[2 * ((i - 1) & 3)];
-        if (t1) stream_e((i - 1) & 1, (int)t1 - 1, (int)s_item[2 * ((i - 1) & 3) + 1]);
-      }
+    // One loop per role with the same barrier count (interval i: C(i+1) | D(i) | E(i-1)), so
+    // that each role's loop-carried registers are live in its own loop only.  A plain
+    // s_barrier behind each wave's own LDS accesses (the roles hand each other LDS rows
+    // only): in a kernel with LDS-DMA the compiler lowers __syncthreads()'s release to
+    // s_waitcnt vmcnt(0), so the streaming waves would drain their stores every tick and
+    // wave 0 would wait for the next tile's prefetch.
+    auto interval_end = [&](int i, unsigned long long w0) __attribute__((always_inline)) -> bool {
       const unsigned long long w1 = SPLIT_NOW();
-      __syncthreads();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       acc_work += w1 - w0;
       acc_wait += SPLIT_NOW() - w1;
-      if (s_item[2 * (i & 3)] == 0) break;              // item i does not exist: all work is done
+      return s_item[2 * (i & 3)] == 0;                  // item i does not exist: all work is done
+    };
+    if (tid < 64) {
+      produce(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      for (int i = 0;; ++i) {
+        const unsigned long long w0 = SPLIT_NOW();
+        produce(i + 1);
+        if (interval_end(i, w0)) break;
+      }
+    } else if (tid < 128) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      for (int i = 0;; ++i) {
+        const unsigned long long w0 = SPLIT_NOW();
+        const uint32_t t1 = s_item[2 * (i & 3)];
+        if (t1) scatter_d(i & 1, (int)min((int64_t)TILE, n - (int64_t)(t1 - 1) * TILE));
+        if (interval_end(i, w0)) break;
+      }
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      for (int i = 0;; ++i) {
+        const unsigned long long w0 = SPLIT_NOW();
+        if (i >= 1) {
+          const uint32_t t1 = s_item[2 * ((i - 1) & 3)];
+          if (t1) stream_e(i - 1, (int)t1 - 1, (int)s_item[2 * ((i - 1) & 3) + 1], true);
+        }
+        if (interval_end(i, w0)) break;
+      }
     }
 #ifdef CRAFT_STAMPS
     if (v.stamps) {
-      uint64_t* row = v.stamps + 8 * (int64_t)blockIdx.x;
+      uint64_t* row = v.stamps + 16 * (int64_t)blockIdx.x;   // 16 words per workgroup
       if (tid == 0) {
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         row[0] = t_beg; row[1] = acc_work; row[2] = acc_wait; row[6] = SPLIT_NOW(); row[7] = acc_sw;
-        (void)xcc;
+        row[8] = acc_vm; row[9] = acc_pub; row[10] = acc_ld; row[11] = acc_dma;
       } else if (tid == 64) {
         row[3] = acc_work; row[4] = acc_wait;
       } else if (tid == 128) {
@@ -430,11 +631,17 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
     (void)acc_work;
     (void)acc_wait;
     (void)acc_sw;
+    (void)acc_pub;
+    (void)acc_vm;
+    (void)acc_ld;
+    (void)acc_dma;
 #undef SPLIT_NOW
   } else {
+    (void)s_out;
+    (void)s_stage;
     // ---- work units (tile t, chunk c) from the queue, one pipeline fill and drain each --------
     for (;;) {
-      if (tid == 0) s_ctrl[0] = (uint32_t)atomicAdd(a.queue, 1ull);
+      if (tid == 0) s_ctrl[0] = (uint32_t)(atomicAdd(a.queue, 1ull) - a.qbase);
       __syncthreads();                                  // also: s_task / rows ready
       const uint32_t u = s_ctrl[0];
       if (u >= n_units) break;                          // workgroup-uniform exit
@@ -459,20 +666,20 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         if (tid < TILE) {
-          load_tile(t, 0);
-          tick_c(k0, 0);                                // C(0) -> buffer 0
+          load_tile(t, 0, std::false_type{});
+          tick_c(k0, 0, false);                         // C(0) -> buffer 0
         }
       }
 
       // the pipeline: interval i runs C(i+1) | D(i) | E(i-1), one barrier each
       if (!want_obs) {
         if (tid < TILE)
-          for (int q = 1; q < nq; ++q) tick_c(k0 + q, q);
+          for (int q = 1; q < nq; ++q) tick_c(k0 + q, q, false);
       } else {
         __syncthreads();                                // C(0) complete
         if (tid < 64) {
           for (int i = 0; i <= nq; ++i) {
-            if (tid < TILE && i + 1 < nq) tick_c(k0 + i + 1, i + 1);
+            if (tid < TILE && i + 1 < nq) tick_c(k0 + i + 1, i + 1, false);
             __syncthreads();
           }
         } else if (tid < 128) {
@@ -482,7 +689,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
           }
         } else {
           for (int i = 0; i <= nq; ++i) {
-            if (i >= 1) stream_e(i - 1, t, k0 + i - 1);
+            if (i >= 1) stream_e(i - 1, t, k0 + i - 1, false);
             __syncthreads();
           }
         }

@@ -145,6 +145,9 @@ struct craft_sim {
   int rollout_threads = 0;          // craft_rollout threads per tile workgroup (0: 8 per env)
   uint8_t* d_sync = nullptr;        // craft_rollout: work-unit counter + per-tile chunk flags
   size_t sync_bytes = 0;
+  bool sync_zeroed = false;         // d_sync zeroed once; then the counter only grows
+  uint64_t queue_next = 0;          // the counter's value at the next launch (every launch adds
+                                    // its units + its grid: one fetch past the end per workgroup)
   std::string last_error;
 };
 
@@ -392,8 +395,8 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
 
 int craft_sim_tune_rollout(craft_sim_t* s, int32_t chunk_ticks, int32_t threads) {
   if (!s) return CRAFT_EINVAL;
-  if (chunk_ticks < 0 || chunk_ticks > 4096)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_rollout: chunk_ticks must be 0..4096");
+  if (chunk_ticks < -1 || chunk_ticks > 4096)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_rollout: chunk_ticks must be -1..4096");
   if (threads != 0 && threads != 128 && threads != 256 && threads != 320 && threads != 384 && threads != 512)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune_rollout: threads must be 0, 128, 256, 320, 384 or 512");
   s->rollout_chunk = chunk_ticks;
@@ -596,7 +599,8 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   // teacher lanes per env: 4 (default) or 1 (CRAFT_TEACH_LANES=1, diagnostic)
   static const int tl = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 1) ? 1 : 4;
   const int tile = craft::kMaxTileEnvs;
-  const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4;
+  const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
+                     CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16;   // + task | frozen words, task_sub, D sync
   hipError_t e = craft::launch_tick_teach(tl, (s->view.C + 31) / 32, s->cfg.window_width, s->view, a, lds,
                                           reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
@@ -636,17 +640,28 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   a.tile_done = reinterpret_cast<uint32_t*>(s->d_sync + 16);
   int tile = 0, threads = 0, split = 0;
   rollout_shape(s, &tile, &threads, &split);
-  // the work-unit queue and hand-off flags: every kernel shape but the split kernel's
-  // continuous pipeline (one unit per tile, observations on), which assigns tiles statically
-  // (CRAFT_UNIT_PIPELINE=1 in the environment: diagnostic, one pipeline per tile instead)
-  static const bool unit_pipeline = getenv("CRAFT_UNIT_PIPELINE") != nullptr;
-  const bool flat = split && a.chunk >= n_ticks && obs != nullptr && !unit_pipeline;
+  // chunk_ticks -1: the split kernel's continuous pipeline (its 3x3 default shape, observations
+  // on; otherwise one unit per tile)
+  const bool flat = s->rollout_chunk == -1 && split && tile == 32 && threads == 512 &&
+                    s->cfg.window_width == 3 && obs != nullptr;
   a.flat = flat ? 1 : 0;
-  if (n_ticks > 0 && !flat)
+  // The work-unit counter is zeroed once and then only grows: a launch hands out units
+  // counter - qbase and ends having added its units + its grid.  Chunked launches (tiles
+  // handed between workgroups) also need zeroed per-tile flags: those zero the whole area.
+  const int64_t n_chunks = n_ticks > 0 ? (n_ticks + a.chunk - 1) / a.chunk : 0;
+  const int64_t units = ((s->n_envs + tile - 1) / tile) * n_chunks;
+  if (n_ticks > 0 && (n_chunks > 1 || !s->sync_zeroed)) {
     HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
+    s->sync_zeroed = true;
+    s->queue_next = 0;
+  }
+  a.qbase = s->queue_next;
+  int64_t grid = 0;
+  a.grid_out = &grid;
   hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, s->view, a, lds_bytes(s, tile, 2, true),
                                        reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");
+  if (grid > 0) s->queue_next += (uint64_t)(units + grid);
   return CRAFT_OK;
 }
 

@@ -34,6 +34,10 @@ namespace craft {
 // Returns false where the reference raises (len(None) on an unreachable target
 // after a reachable one, base.py:31): the forward BFS then runs until its
 // frontier is empty, so `claimed` holds every reachable target.
+// A level's states face a target where they stand on F_a = shift(tgt, -d_a) (the
+// cell ahead in their direction a is a target), so the level loop only tests
+// nxt_a & F_a; the faced targets themselves are formed on the rare levels that
+// have any.
 // One lane per query (LANES = 1): the same forward and backward passes, the four
 // actions of a level in one lane.
 template <int NW>
@@ -42,9 +46,12 @@ __device__ bool bfs_closest_1(const Bits<NW>& occ, const Bits<NW>& tgt, const Bi
                               bool want_action) {
   const int dl[4] = {-1, 1, -H, H};   // DOWN, UP, LEFT, RIGHT in x-major cell index
   const Bits<NW> fr = bandn(valid, occ);
-  Bits<NW> blk[4];
+  Bits<NW> blk[4], fa[4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a) blk[a] = bshift(occ, -dl[a]);   // blk[a][p] = occ[p + dl[a]]
+  for (int a = 0; a < 4; ++a) {
+    blk[a] = bshift(occ, -dl[a]);     // blk[a][p] = occ[p + dl[a]]
+    fa[a] = bshift(tgt, -dl[a]);      // fa[a][p] = tgt[p + dl[a]]
+  }
   first_action = -1;
   path_len = -1;
   Bits<NW> claimed = bzero<NW>();
@@ -61,30 +68,51 @@ __device__ bool bfs_closest_1(const Bits<NW>& occ, const Bits<NW>& tgt, const Bi
 #pragma unroll
   for (int a = 0; a < 4; ++a) V[a] = (a == d0) ? bbit<NW>(p0) : bzero<NW>();
   Bits<NW> U = bbit<NW>(p0);
-  for (int depth = 1; bany(bandn(tgt, claimed)); ++depth) {
-    Bits<NW> nU = bzero<NW>(), hit = bzero<NW>();
+  const bool open = bany(bandn(tgt, claimed));   // some target not yet claimed
+  for (int depth = 1; open && L < 0; ++depth) {
+    Bits<NW> nU = bzero<NW>(), nx[4];
+    uint32_t face = 0;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const Bits<NW> nxt = bandn(bor(band(bshift(U, dl[a]), fr), band(U, blk[a])), V[a]);
-      V[a] = bor(V[a], nxt);
-      nU = bor(nU, nxt);
-      hit = bor(hit, band(bshift(nxt, dl[a]), tgt));
+      nx[a] = bandn(bor(band(bshift(U, dl[a]), fr), band(U, blk[a])), V[a]);
+      V[a] = bor(V[a], nx[a]);
+      nU = bor(nU, nx[a]);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) face |= nx[a].w[i] & fa[a].w[i];
     }
     if (!bany(nU)) break;                  // every reachable state visited
-    hit = bandn(hit, claimed);
-    if (bany(hit)) {
-      claimed = bor(claimed, hit);
-      if (L < 0) {
+    if (face) {
+      Bits<NW> hit = bzero<NW>();
+#pragma unroll
+      for (int a = 0; a < 4; ++a) hit = bor(hit, band(bshift(nx[a], dl[a]), tgt));
+      hit = bandn(hit, claimed);
+      if (bany(hit)) {
+        claimed = bor(claimed, hit);
         L = depth;
         chosen = blowest(hit);
+        break;                             // L and the chosen target are known
       }
     }
     U = nU;
   }
   if (L < 0) return true;                  // no target at all, or none reachable: None
   path_len = L;
-  const Bits<NW> unreached = bandn(tgt, claimed);
-  if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  if (bany(bandn(tgt, claimed))) {
+    // reachability of the other targets (base.py:31), as in bfs_closest below
+    Bits<NW> R = bor(bor(bor(V[0], V[1]), bor(V[2], V[3])), bbit<NW>(p0));
+    for (;;) {
+      Bits<NW> adj = bzero<NW>();
+#pragma unroll
+      for (int a = 0; a < 4; ++a) adj = bor(adj, bshift(R, dl[a]));
+      claimed = bor(claimed, band(adj, tgt));
+      if (!bany(bandn(tgt, claimed))) break;
+      const Bits<NW> grow = bandn(band(adj, fr), R);
+      if (!bany(grow)) break;
+      R = bor(R, grow);
+    }
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  }
   if (L == 0 || !want_action) return true;
   Bits<NW> G[4];                           // reverse BFS from the states facing `chosen`
 #pragma unroll
@@ -139,7 +167,9 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
   const int dla = ql == 0 ? -1 : ql == 1 ? 1 : ql == 2 ? -H : H;   // this lane's action
   const Bits<NW> fr = bandn(valid, occ);
   const Bits<NW> blk = bshift_var(occ, -dla);                         // blk[p] = occ[p + dla]
+  const Bits<NW> fa = bshift_var(tgt, -dla);                          // fa[p] = tgt[p + dla]
   const int dl0 = d0 == 0 ? -1 : d0 == 1 ? 1 : d0 == 2 ? -H : H;
+  const uint32_t qsh = __lane_id() & ~3u;                             // this quad's lanes in a ballot
   first_action = -1;
   path_len = -1;
   Bits<NW> claimed = bzero<NW>();
@@ -154,26 +184,45 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
   }
   Bits<NW> V = (ql == d0) ? bbit<NW>(p0) : bzero<NW>();   // visited states of direction ql
   Bits<NW> U = bbit<NW>(p0);
-  for (int depth = 1; bany(bandn(tgt, claimed)); ++depth) {
+  const bool open = bany(bandn(tgt, claimed));   // some target not yet claimed (quad-uniform)
+  for (int depth = 1; open && L < 0; ++depth) {
     const Bits<NW> nxt = bandn(bor(band(bshift_var(U, dla), fr), band(U, blk)), V);
     V = bor(V, nxt);
     const Bits<NW> nU = quad_or(nxt);
-    Bits<NW> hit = quad_or(band(bshift_var(nxt, dla), tgt));
     if (!bany(nU)) break;                  // every reachable state visited
-    hit = bandn(hit, claimed);
-    if (bany(hit)) {
-      claimed = bor(claimed, hit);
-      if (L < 0) {
+    uint32_t face = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) face |= nxt.w[i] & fa.w[i];
+    if ((uint32_t)(__ballot(face != 0) >> qsh) & 0xfu) {   // some lane of the quad faces a target
+      const Bits<NW> hit = bandn(quad_or(band(bshift_var(nxt, dla), tgt)), claimed);
+      if (bany(hit)) {
+        claimed = bor(claimed, hit);
         L = depth;
         chosen = blowest(hit);
+        break;                             // L and the chosen target are known
       }
     }
     U = nU;
   }
   if (L < 0) return true;                  // no target at all, or none reachable: None
   path_len = L;
-  const Bits<NW> unreached = bandn(tgt, claimed);
-  if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  if (bany(bandn(tgt, claimed))) {
+    // Which of the other targets are reachable at all (base.py:31 raises on an unreachable
+    // target after a reachable one): a target is faced from any reachable position next
+    // to it (a blocked move turns in place), so flood the free cells from the positions
+    // visited so far until every target is claimed or nothing new is reached.
+    Bits<NW> R = bor(quad_or(V), bbit<NW>(p0));
+    for (;;) {
+      const Bits<NW> adj = quad_or(bshift_var(R, dla));          // cells next to R
+      claimed = bor(claimed, band(adj, tgt));
+      if (!bany(bandn(tgt, claimed))) break;
+      const Bits<NW> grow = bandn(band(adj, fr), R);
+      if (!bany(grow)) break;
+      R = bor(R, grow);
+    }
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  }
   if (L == 0 || !want_action) return true;
   // reverse BFS from the states facing `chosen`; G = this level's states of direction
   // ql, V reused as the reverse-visited set
@@ -199,15 +248,68 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
   return true;
 }
 
+// Lane s of the quad's value, in every lane of the quad (DPP quad_perm [s,s,s,s]).
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t x, int s) {
+  switch (s) {
+    case 0: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x00, 0xF, 0xF, false);
+    case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x55, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xAA, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xFF, 0xF, 0xF, false);
+  }
+}
+
+
+// Occupancy and `kind` target sets of a grid row (kind ids, 4 cells per 32-bit word
+// of row32, nq words) minus the cells set in m: SWAR byte tests on whole words
+// (nonzero byte: ((w & 0x7f..) + 0x7f..) | w has bit 7 set; equal byte: the same on
+// w ^ kind), 32 cells per result word, no per-cell work.  With LANES = 4 the quad
+// splits the words (lane ql builds words ql, ql + 4, ...) and broadcasts them.
+template <int NW, int LANES>
+__device__ __forceinline__ void grid_bits(const uint32_t* row32, int nq, const uint32_t (&m)[8],
+                                          uint32_t kind, int ql, const Bits<NW>& valid,
+                                          Bits<NW>& occ, Bits<NW>& tgt) {
+  constexpr int PER = (NW + LANES - 1) / LANES;   // result words per lane
+  const uint32_t k4 = kind * 0x01010101u;
+  uint32_t po[PER], pt[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int w = ql + j * LANES;
+    uint32_t o = 0u, t = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = 8 * w + k;
+      const uint32_t d = (w < NW && q < nq) ? row32[q] : 0u;
+      const uint32_t nz = nonzero_bytes(d);
+      const uint32_t eq = zero_bytes(d ^ k4);
+      o |= byte_tops(nz) << (4 * k);
+      t |= byte_tops(eq) << (4 * k);
+    }
+    uint32_t clr = 0u;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) clr = (i == w) ? m[i] : clr;
+    po[j] = o & ~clr;
+    pt[j] = t & ~clr;
+  }
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t oi = LANES == 1 ? po[i / LANES] : quad_bcast(po[i / LANES], i % LANES);
+    const uint32_t ti = LANES == 1 ? pt[i / LANES] : quad_bcast(pt[i / LANES], i % LANES);
+    occ.w[i] = oi & valid.w[i];
+    tgt.w[i] = ti & oi & valid.w[i];
+  }
+}
+
 // DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for one env, LANES
 // lanes of a quad-aligned group (lane ql of the group).  Its current grid is row32
 // (kind ids, x-major, as 32-bit words; NW*8 words at most) minus the cells set in m
 // (cleared this episode; all zero when the row is already current), its inventory
-// iv, its agent s, the task `task`.  Returns the action, or -2 where the reference
+// iv, its agent s, the task `task`; task_tab / task_sub are the handle's task tables
+// (v.task_tab / v.task_sub, or copies in LDS).  Returns the action, or -2 where the reference
 // raises (err_out = CRAFT_ETEACHER).  With want_len, len_out receives
 // len(find_closest_resources(task.arg)) (-1: no target, -2: the reference raises).
 template <int NW, int LANES>
-__device__ __forceinline__ int teach_env(const SimView& v, const uint32_t* row32, const uint32_t (&m)[8],
+__device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_tab, const int32_t* task_sub,
+                                         const uint32_t* row32, const uint32_t (&m)[8],
                                          const uint8_t* iv, const Agent& s, int task, int ql,
                                          bool want_len, int& len_out, int& err_out) {
   const int H = v.H, C = v.C;
@@ -219,7 +321,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint32_t* row32
   const int facing = kind_at((s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir)));
 
   auto sat = [&](int t) -> int {       // satisfies(), craft.py:285-294
-    const uint32_t tt = v.task_tab[t];
+    const uint32_t tt = task_tab[t];
     const int goal = tt & 0xf, arg = (tt >> 4) & 0xff;
     if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) return iv[arg] > 0;
     if (goal == CRAFT_GOAL_GO) return facing == arg;
@@ -232,32 +334,15 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint32_t* row32
     const int nb = min(32, max(0, C - w * 32));
     valid.w[w] = nb >= 32 ? ~0u : ((1u << nb) - 1u);
   }
-  // Occupancy and per-kind target bitsets of the current grid: the row is read as
-  // dwords in a fully unrolled loop so every bit position is static (no per-cell
-  // dependent loads, no dynamic indexing).
   const int nq = (C + 3) >> 2;
-  auto grids = [&](int kind, Bits<NW>& occ, Bits<NW>& tgt) {
-    occ = bzero<NW>();
-    tgt = bzero<NW>();
-#pragma unroll
-    for (int q = 0; q < NW * 8; ++q) {
-      if (q < nq) {
-        const uint32_t w = row32[q];
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int c = 4 * q + b;
-          const uint32_t k = (w >> (8 * b)) & 0xffu;
-          const bool cleared = (m[c >> 5] >> (c & 31)) & 1u;
-          const uint32_t bit = (k != 0 && !cleared) ? (1u << (c & 31)) : 0u;
-          occ.w[c >> 5] |= bit;
-          tgt.w[c >> 5] |= (k == (uint32_t)kind) ? bit : 0u;
-        }
-      }
-    }
-  };
   auto closest = [&](int kind, int& fa, int& len, bool want_action) -> bool {
     Bits<NW> occ, tgt;
-    grids(kind, occ, tgt);
+    grid_bits<NW, LANES>(row32, nq, m, (uint32_t)kind, ql, valid, occ, tgt);
+#ifdef CRAFT_ABL_NOBFS
+    fa = (int)(occ.w[0] ^ tgt.w[NW - 1]) & 3;             // ablation build only: no BFS
+    len = 1;
+    return true;
+#endif
     return bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y, s.dir, ql, fa, len, want_action);
   };
   int leaf_kind = -1, leaf_fa = -1, leaf_len = -1;
@@ -269,9 +354,9 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint32_t* row32
   int node = task;
   if (sat(node) != 1) {
     for (int guard = 0; guard < CRAFT_MAX_TASKS; ++guard) {
-      const int nsub = (v.task_tab[node] >> 12) & 0xf;
+      const int nsub = (task_tab[node] >> 12) & 0xf;
       if (nsub == 0) break;
-      const int32_t* sub = v.task_sub + CRAFT_MAX_SUBTASKS * node;
+      const int32_t* sub = task_sub + CRAFT_MAX_SUBTASKS * node;
       int chosen = sub[nsub - 1];
       bool last = true;
       for (int q = 0; q + 1 < nsub; ++q)
@@ -280,7 +365,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint32_t* row32
       node = chosen;
     }
     if (!err) {
-      const uint32_t lt = v.task_tab[node];
+      const uint32_t lt = task_tab[node];
       const int goal = lt & 0xf, arg = (lt >> 4) & 0xff;
       if (goal == CRAFT_GOAL_USE) {
         action = CRAFT_USE;
@@ -300,7 +385,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint32_t* row32
   if (err) action = -2;                // where the reference raises
   err_out = err;
   if (want_len) {
-    const int arg = (v.task_tab[task] >> 4) & 0xff;
+    const int arg = (task_tab[task] >> 4) & 0xff;
     int fa = leaf_fa, len = leaf_len;
     bool ok = leaf_ok;
     if (arg != leaf_kind) {               // the teacher's BFS already answered get[X]'s go[X]

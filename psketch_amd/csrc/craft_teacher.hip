@@ -24,6 +24,14 @@ struct TeachArgs {
 // what bounds a large one (launch_teacher picks by batch size).
 template <int NW, int LANES>
 __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
+  // the task tables in LDS: the hint-tree walk reads them in a dependent chain
+  __shared__ uint16_t s_tab[CRAFT_MAX_TASKS];
+  __shared__ int32_t s_sub[CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS];
+  for (int t = threadIdx.x; t < v.n_tasks * CRAFT_MAX_SUBTASKS; t += blockDim.x) {
+    if (t < v.n_tasks) s_tab[t] = v.task_tab[t];
+    s_sub[t] = v.task_sub[t];
+  }
+  __syncthreads();
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
   const int ql = LANES == 4 ? (threadIdx.x & 3) : 0;
   if (i >= a.n) return;                  // lane-group-uniform: a group never straddles two items
@@ -71,7 +79,8 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   const uint8_t* iv = reinterpret_cast<const uint8_t*>(v.inv + 2 * slot);
   const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
   int len = -1, err = 0;
-  const int action = teach_env<NW, LANES>(v, row32, m, iv, s, task, ql, a.len_out != nullptr, len, err);
+  const int action = teach_env<NW, LANES>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
+                                          len, err);
   if (lead) {
     if (err) latch_error(v.err, err, slot);
     a.act_out[i] = action;

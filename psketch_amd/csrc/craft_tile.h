@@ -37,6 +37,8 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
   uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.bytes);   // TL > 0: [TILE] task | frozen << 8
+  int32_t* s_tsub = reinterpret_cast<int32_t*>(s_tinfo + TILE);           // TL > 0: task_sub copy
+  uint32_t* s_dsync = reinterpret_cast<uint32_t*>(s_tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS);   // TL > 0
 
   const int tid = threadIdx.x;
   const int64_t env0 = (int64_t)blockIdx.x * TILE;
@@ -48,6 +50,10 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
   // ---- A + C: wave 0, one lane per env ------------------------------------------------------
   if (tid < TILE) {
     for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
+    if (TL > 0) {
+      for (int t = tid; t < v.n_tasks * CRAFT_MAX_SUBTASKS; t += TILE) s_tsub[t] = v.task_sub[t];
+      if (tid == 0) *s_dsync = 0u;
+    }
     for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += TILE) s_rc[t] = v.rcw[t];
 
     int64_t slot = 0, dslot = 0;
@@ -264,10 +270,20 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
 
   // ---- D: scatter the observation's non-zero bytes ---------------------------------------------
   if (want_obs && tid < kThreads) scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
-  if (want_obs) __syncthreads();
+  if (TL == 0) {
+    if (want_obs) __syncthreads();
+  } else if (want_obs && tid < kThreads) {
+    // D -> E among the tick's 4 waves only (an LDS arrival counter), so the teacher waves
+    // start right after C instead of waiting out the scatter at a workgroup barrier
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((tid & 63) == 0) __hip_atomic_fetch_add(s_dsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(s_dsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)(kThreads / 64))
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   STAMP(5);
 
-  if (TL > 0 && tid >= kThreads) {
+  if constexpr (TL > 0) if (tid >= kThreads) {
     // ---- T: DemonstrationTeacher on the new state (teachers/demonstration.py:9-30) from the
     // grid row the tick left in LDS (cleared cells already applied), overlapping E ----------
     const int u = tid - kThreads, e = u / TL, ql = u % TL;
@@ -278,12 +294,16 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
       if (ag && ((ti >> 8) & 1u)) {
         action = -1;                                      // frozen: the trainer's label for a done env
       } else if (ag) {
+#ifdef CRAFT_ABL_NOTEACH
+        action = CRAFT_STOP;                              // ablation build only: no teacher work
+      } else if (false) {
+#endif
         Agent s{};
         s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int len = -1, err = 0;
-        action = teach_env<NW, TL>(v, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS), m0,
-                                   s_inv + e * kInvStride, s, s.task, ql, false, len, err);
+        action = teach_env<NW, TL>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS),
+                                   m0, s_inv + e * kInvStride, s, s.task, ql, false, len, err);
         if (err && ql == 0) latch_error(v.err, err, i);
       }
       if (ql == 0) a.label[i] = action;

@@ -82,8 +82,9 @@ class CraftSim:
 
     def tune_rollout(self, chunk_ticks=0, threads=0):
         """Ticks per dynamically scheduled work unit of rollout() (0 = the whole
-        launch, the default) and threads per tile workgroup (0 = 8 per env);
-        results are identical for every setting."""
+        launch, the default; -1 = one continuous pipeline per workgroup across
+        its tiles) and threads per tile workgroup (0 = the library's default
+        shape); results are identical for every setting."""
         self._check(N.lib().craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
                     "craft_sim_tune_rollout")
 

@@ -410,7 +410,11 @@ def test_lockstep_other_geometries(oracle_mod, world, W):
     ("craft_16x16_w7", 16, 0, "f32", False, False, 0, 3, 0),
     ("craft_16x16_w7", 16, 32, "f32", True, False, 0, 3, 256),
     ("craft_medium", 8, 64, "f32", True, True, 1, 9, 0),
-    ("craft_medium", 8, 64, "f32", True, True, 0, 9, 256)])
+    ("craft_medium", 8, 64, "f32", True, True, 0, 9, 256),
+    # chunk -1: the continuous pipeline (prefetched tile switches, deferred outputs)
+    ("craft_medium_12x12", 12, 0, "f32", True, False, -1, 3, 0),
+    ("craft_medium_12x12", 12, 0, "bf16", False, True, -1, 16, 0),
+    ("craft_medium_12x12", 12, 0, "u8", True, True, -1, 9, 0)])
 def test_multi_tick_rollout_equals_steps(world, W, tile, fmt, autoreset, given, chunk, R, threads):
     """craft_rollout(K ticks) == K craft_step calls: observation / reward / done /
     success rings, final states and episode statistics, bit for bit; several
@@ -497,6 +501,7 @@ def test_empty_and_single_env_calls(gpu):
 @pytest.mark.parametrize("launches,R,chunk", [
     ((32,), 16, 0),          # the bench's default launch
     ((20, 13), 16, 0),       # the driver's --steps 20 launch, then a ragged one
+    ((20, 3, 32), 16, -1),   # the continuous pipeline, incl. launches shorter than its prefetch
     ((32,), 32, 4),          # chunked units, ring >= launch: write-through state hand-off
     ((24,), 8, 3)])          # chunked units, ring < launch: full release between units
 def test_bench_rollout_equals_steps_at_full_size(launches, R, chunk):
