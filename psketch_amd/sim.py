@@ -61,6 +61,7 @@ class CraftSim:
                                          ctypes.byref(handle)), what="craft_sim_create")
         self._h = handle
         self.obs_format, self.obs_dtype = "f32", torch.float32
+        self._rollout_cache = None
 
     # ---- lifetime ---------------------------------------------------------------
     def close(self):
@@ -112,6 +113,7 @@ class CraftSim:
         code, dtype = self._OBS_FORMATS[fmt]
         self._check(N.lib().craft_sim_set_obs_format(self._h, code), "craft_sim_set_obs_format")
         self.obs_format, self.obs_dtype = fmt, dtype
+        self._rollout_cache = None
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
@@ -279,6 +281,17 @@ class CraftSim:
         n = self.n_envs
         if n_ticks < 0:
             raise ValueError("n_ticks must be >= 0")
+        if actions is None:
+            # the same output tensors as the last call (a benchmark or trainer loop): their checks
+            # still hold, so only the launch arguments change
+            c = self._rollout_cache
+            if c is not None and c[0] is obs and c[1] is reward and c[2] is done and c[3] is success \
+                    and c[4] == self._ring_sig(obs, reward, done, success):
+                self._check(self._rollout_fn(self._h, None, ctypes.c_uint64(seed & (2**64 - 1)),
+                                             int(tick0), int(n_ticks),
+                                             N.STEP_AUTORESET if autoreset else 0, c[5], c[6], c[7],
+                                             c[8], c[9], self._stream()), "craft_rollout")
+                return obs
         ring = None
         for name, t in (("obs", obs), ("reward", reward), ("done", done), ("success", success)):
             if t is not None:
@@ -295,12 +308,22 @@ class CraftSim:
         a = None
         if actions is not None:
             a = self._i32(actions, n * n_ticks)
-        self._check(N.lib().craft_rollout(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
-                                          int(tick0), int(n_ticks),
-                                          N.STEP_AUTORESET if autoreset else 0, _ptr(obs),
-                                          int(ring or 1), _ptr(reward), _ptr(done), _ptr(success),
-                                          self._stream()), "craft_rollout")
+        self._rollout_fn = N.lib().craft_rollout
+        self._check(self._rollout_fn(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
+                                     int(tick0), int(n_ticks),
+                                     N.STEP_AUTORESET if autoreset else 0, _ptr(obs),
+                                     int(ring or 1), _ptr(reward), _ptr(done), _ptr(success),
+                                     self._stream()), "craft_rollout")
+        if a is None:
+            self._rollout_cache = (obs, reward, done, success, self._ring_sig(obs, reward, done, success),
+                                   _ptr(obs), int(ring or 1), _ptr(reward), _ptr(done), _ptr(success))
         return obs
+
+    @staticmethod
+    def _ring_sig(*ts):
+        """Storage and shape of each output ring (a tensor resized or re-pointed in place since
+        the last call no longer matches)."""
+        return tuple((t.data_ptr(), t.shape) if t is not None else None for t in ts)
 
     def stats(self, reset=False, out=None):
         """Device int64[3] {successes, episodes ended, env-steps}."""

@@ -544,3 +544,22 @@ def test_bench_rollout_equals_steps_at_full_size(launches, R, chunk):
     assert host(a.stats())[2] == n * sum(launches)
     a.check()
     b.check()
+
+
+def test_rollout_fast_path_revalidates_resized_rings():
+    """rollout() skips re-checking output rings it has seen unchanged; a ring resized
+    (or re-pointed) in place since the last call is checked again and refused."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 16)
+    n = 256
+    sim = sim_with_pool(world, n, pool)
+    sim.reset(*synthetic_specs(pool, 12, 12, n, 0, seed=1, task_ids=[t.id for t in tm.dataset_tasks()]))
+    ring = torch.empty((4, n, sim.n_features), dtype=torch.float32, device="cuda")
+    done = torch.empty((4, n), dtype=torch.uint8, device="cuda")
+    sim.rollout(3, tick0=0, obs=ring, done=done)
+    sim.rollout(3, tick0=3, obs=ring, done=done)          # the cached path
+    ring.resize_(4, n // 2, sim.n_features)
+    with pytest.raises(ValueError):
+        sim.rollout(3, tick0=6, obs=ring, done=done)
+    sim.check()
