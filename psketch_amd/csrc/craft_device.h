@@ -33,6 +33,7 @@ enum Mode { MODE_TICK = 0, MODE_TRANSITION = 1, MODE_OBSERVE = 2, MODE_RESET = 3
 
 struct SimView {
   const uint8_t* pool;
+  const uint8_t* pool_conn;   // [P]: 1 = the free cells of pool row p form one 4-connected component
   uint64_t* state;
   uint32_t* init;
   uint4* inv;

@@ -124,6 +124,8 @@ __global__ __launch_bounds__(256) void scenario_kernel(SimView v, ScenarioArgs a
     latch_error(v.err, CRAFT_EINVARIANT, a.id0 + s);
     c = 0;
   }
+  // every accepted placement kept the free cells one component (acceptance test (1))
+  const_cast<uint8_t*>(v.pool_conn)[a.first + s] = failed ? 0 : 1;
   if (a.init_out) {
     a.init_out[2 * s] = c / H;
     a.init_out[2 * s + 1] = c % H;

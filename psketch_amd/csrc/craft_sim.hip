@@ -129,6 +129,7 @@ struct craft_sim {
   int64_t n_envs = 0, env_base = 0, n_tiles = 0;
   int32_t pool_capacity = 0, pool_count = 0;
   uint8_t* d_pool = nullptr;
+  uint8_t* d_pool_conn = nullptr;   // per pool row: free cells 4-connected (teacher shortcut)
   uint32_t* d_rcw = nullptr;
   uint64_t* d_state = nullptr;
   uint32_t* d_init = nullptr;
@@ -327,6 +328,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     if ((e = hipMemset((ptr), 0, (bytes))) != hipSuccess) return cleanup(e, #ptr); \
   } while (0)
   ALLOC(s->d_pool, (size_t)pool_capacity * CS);
+  ALLOC(s->d_pool_conn, (size_t)pool_capacity + 16);
   ALLOC(s->d_state, sizeof(uint64_t) * n_envs);
   ALLOC(s->d_init, sizeof(uint32_t) * n_envs);
   ALLOC(s->d_inv, 2 * sizeof(uint4) * n_envs);
@@ -348,6 +350,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
 
   SimView& v = s->view;
   v.pool = s->d_pool;
+  v.pool_conn = s->d_pool_conn;
   v.state = s->d_state;
   v.init = s->d_init;
   v.inv = s->d_inv;
@@ -416,6 +419,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   if (!s) return CRAFT_OK;
   (void)hipSetDevice(s->device);
   (void)hipFree(s->d_pool);
+  (void)hipFree(s->d_pool_conn);
   (void)hipFree(s->d_state);
   (void)hipFree(s->d_init);
   (void)hipFree(s->d_inv);
@@ -479,6 +483,7 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
   if ((int64_t)first + count > s->pool_capacity) return fail(s, CRAFT_ERANGE, "craft_pool_load: beyond pool capacity");
   const int W = s->cfg.width, H = s->cfg.height, C = W * H, CS = s->view.CS;
   std::vector<uint8_t> staged((size_t)count * CS, 0);
+  std::vector<uint8_t> conn((size_t)count, 0);
   for (int p = 0; p < count; ++p) {
     const uint8_t* g = grids + (size_t)p * C;
     for (int c = 0; c < C; ++c) {
@@ -490,10 +495,35 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
                                              " has an open border cell (make_data.py:108-112 builds a boundary ring)");
     }
     std::memcpy(staged.data() + (size_t)p * CS, g, C);
+    // are the free cells one 4-connected component?  Cells are only ever cleared next to the
+    // agent, so every env grid of this scenario then keeps its free cells connected, and the
+    // teacher reads target reachability off the grid instead of flooding it (craft_teach.h)
+    std::vector<int> stack;
+    std::vector<uint8_t> seen(C, 0);
+    int n_free = 0, first_free = -1;
+    for (int c = 0; c < C; ++c)
+      if (g[c] == 0) { ++n_free; if (first_free < 0) first_free = c; }
+    int n_seen = 0;
+    if (first_free >= 0) { stack.push_back(first_free); seen[first_free] = 1; }
+    while (!stack.empty()) {
+      const int c = stack.back();
+      stack.pop_back();
+      ++n_seen;
+      const int x = c / H, y = c % H;
+      const int nb[4][2] = {{x, y - 1}, {x, y + 1}, {x - 1, y}, {x + 1, y}};
+      for (auto& q : nb) {
+        if (q[0] < 0 || q[0] >= W || q[1] < 0 || q[1] >= H) continue;
+        const int d = q[0] * H + q[1];
+        if (!seen[d] && g[d] == 0) { seen[d] = 1; stack.push_back(d); }
+      }
+    }
+    conn[p] = n_seen == n_free ? 1 : 0;
   }
   HIP_TRY(s, hipSetDevice(s->device));
-  if (count)
+  if (count) {
     HIP_TRY(s, hipMemcpy(s->d_pool + (size_t)first * CS, staged.data(), staged.size(), hipMemcpyHostToDevice));
+    HIP_TRY(s, hipMemcpy(s->d_pool_conn + first, conn.data(), count, hipMemcpyHostToDevice));
+  }
   if (first + count > s->pool_count) s->pool_count = first + count;
   s->view.pool_count = s->pool_count;
   return CRAFT_OK;

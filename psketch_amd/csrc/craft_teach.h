@@ -43,7 +43,7 @@ namespace craft {
 template <int NW>
 __device__ bool bfs_closest_1(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
                               int H, int p0, int d0, int& first_action, int& path_len,
-                              bool want_action) {
+                              bool want_action, bool conn) {
   const int dl[4] = {-1, 1, -H, H};   // DOWN, UP, LEFT, RIGHT in x-major cell index
   const Bits<NW> fr = bandn(valid, occ);
   Bits<NW> blk[4], fa[4];
@@ -97,7 +97,15 @@ __device__ bool bfs_closest_1(const Bits<NW>& occ, const Bits<NW>& tgt, const Bi
   }
   if (L < 0) return true;                  // no target at all, or none reachable: None
   path_len = L;
-  if (bany(bandn(tgt, claimed))) {
+  if (bany(bandn(tgt, claimed)) && conn && btest(fr, p0)) {
+    // every free cell is reachable (bfs_closest below): the targets next to one
+    Bits<NW> adj = bzero<NW>();
+#pragma unroll
+    for (int a = 0; a < 4; ++a) adj = bor(adj, bshift(fr, dl[a]));
+    claimed = bor(claimed, band(adj, tgt));
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  } else if (bany(bandn(tgt, claimed))) {
     // reachability of the other targets (base.py:31), as in bfs_closest below
     Bits<NW> R = bor(bor(bor(V[0], V[1]), bor(V[2], V[3])), bbit<NW>(p0));
     for (;;) {
@@ -162,8 +170,9 @@ __device__ __forceinline__ Bits<NW> quad_or(const Bits<NW>& a) {
 template <int NW, int LANES>
 __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
                             int H, int p0, int d0, int ql, int& first_action, int& path_len,
-                            bool want_action = true) {
-  if (LANES == 1) return bfs_closest_1<NW>(occ, tgt, valid, H, p0, d0, first_action, path_len, want_action);
+                            bool want_action, bool conn) {
+  if (LANES == 1)
+    return bfs_closest_1<NW>(occ, tgt, valid, H, p0, d0, first_action, path_len, want_action, conn);
   const int dla = ql == 0 ? -1 : ql == 1 ? 1 : ql == 2 ? -H : H;   // this lane's action
   const Bits<NW> fr = bandn(valid, occ);
   const Bits<NW> blk = bshift_var(occ, -dla);                         // blk[p] = occ[p + dla]
@@ -206,7 +215,14 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
   }
   if (L < 0) return true;                  // no target at all, or none reachable: None
   path_len = L;
-  if (bany(bandn(tgt, claimed))) {
+  if (bany(bandn(tgt, claimed)) && conn && btest(fr, p0)) {
+    // The free cells are one component (the scenario's are, and cells are only ever cleared
+    // next to the agent): every free cell is reachable, so a target is reachable iff it has
+    // a free neighbour -- no flood fill.
+    claimed = bor(claimed, band(quad_or(bshift_var(fr, dla)), tgt));
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  } else if (bany(bandn(tgt, claimed))) {
     // Which of the other targets are reachable at all (base.py:31 raises on an unreachable
     // target after a reachable one): a target is faced from any reachable position next
     // to it (a blocked move turns in place), so flood the free cells from the positions
@@ -303,7 +319,8 @@ __device__ __forceinline__ void grid_bits(const uint32_t* row32, int nq, const u
 // lanes of a quad-aligned group (lane ql of the group).  Its current grid is row32
 // (kind ids, x-major, as 32-bit words; NW*8 words at most) minus the cells set in m
 // (cleared this episode; all zero when the row is already current), its inventory
-// iv, its agent s, the task `task`; task_tab / task_sub are the handle's task tables
+// iv, its agent s, the task `task`; conn: the scenario's free cells are one component
+// (pool_conn); task_tab / task_sub are the handle's task tables
 // (v.task_tab / v.task_sub, or copies in LDS).  Returns the action, or -2 where the reference
 // raises (err_out = CRAFT_ETEACHER).  With want_len, len_out receives
 // len(find_closest_resources(task.arg)) (-1: no target, -2: the reference raises).
@@ -311,7 +328,7 @@ template <int NW, int LANES>
 __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_tab, const int32_t* task_sub,
                                          const uint32_t* row32, const uint32_t (&m)[8],
                                          const uint8_t* iv, const Agent& s, int task, int ql,
-                                         bool want_len, int& len_out, int& err_out) {
+                                         bool want_len, int& len_out, int& err_out, bool conn) {
   const int H = v.H, C = v.C;
   auto kind_at = [&](int c) -> int {
     const uint32_t w = row32[c >> 2];
@@ -343,7 +360,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
     len = 1;
     return true;
 #endif
-    return bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y, s.dir, ql, fa, len, want_action);
+    return bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y, s.dir, ql, fa, len, want_action, conn);
   };
   int leaf_kind = -1, leaf_fa = -1, leaf_len = -1;
   bool leaf_ok = true;

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
   int len = -1, err = 0;
   const int action = teach_env<NW, LANES>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
-                                          len, err);
+                                          len, err, v.pool_conn[s.scen] != 0);
   if (lead) {
     if (err) latch_error(v.err, err, slot);
     a.act_out[i] = action;

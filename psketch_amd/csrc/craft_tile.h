@@ -108,6 +108,8 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
       }
     }
     uint8_t* g = s_grid + tid * v.GS;
+    uint32_t conn = 0;                                     // TL > 0: the scenario's free cells connected
+    if (TL > 0 && live) conn = v.pool_conn[s.scen];
     if (live) {
       // the env's scenario grid: CS/16 independent 16-byte loads (L2-resident pool)
       const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
     }
     if ((MODE == MODE_TICK || MODE == MODE_TRANSITION) && a.code && tid < nE) a.code[env0 + tid] = (int8_t)code;
     s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
-    if (TL > 0) s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8);
+    if (TL > 0) s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9);
     if (MODE == MODE_TICK) {
       // episode statistics: one partial-sum row per workgroup (uncontended)
       const uint64_t bs = __ballot(live && counted && d && succ == 1);
@@ -303,7 +305,8 @@ __global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, T
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int len = -1, err = 0;
         action = teach_env<NW, TL>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS),
-                                   m0, s_inv + e * kInvStride, s, s.task, ql, false, len, err);
+                                   m0, s_inv + e * kInvStride, s, s.task, ql, false, len, err,
+                                   ((ti >> 9) & 1u) != 0);
         if (err && ql == 0) latch_error(v.err, err, i);
       }
       if (ql == 0) a.label[i] = action;
