@@ -495,25 +495,27 @@ static hipError_t launch_rollout_split_one(const SimView& v, const RolloutArgs& 
   const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
   if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
   constexpr int WPE = WIN == 3 ? CRAFT_SPLIT_WPE : 2;
-  const size_t lds = (size_t)split_lds_bytes(TILE, v.GS, v.F, v.CS);
   // the continuous-pipeline instantiation exists for the default 3x3 shape only
   constexpr bool kFlatShape = WIN == 3 && TILE == 32 && NT == 512;
-  auto kern = (kFlatShape && a.flat) ? rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, kFlatShape>
-                                     : rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>;
+  const bool flat = kFlatShape && a.flat;
+  const size_t lds = (size_t)split_lds_bytes(TILE, v.GS, v.F, v.CS, flat);
+  auto kern = flat ? rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, kFlatShape>
+                   : rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>;
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  static int resident = 0;
-  static size_t resident_lds = 0;
-  if (resident == 0 || resident_lds != lds) {
+  static int resident_of[2] = {0, 0};                 // per instantiation (flat or not)
+  static size_t resident_lds[2] = {0, 0};
+  int& resident = resident_of[flat ? 1 : 0];
+  if (resident == 0 || resident_lds[flat ? 1 : 0] != lds) {
     int per_cu = 0, dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
       cus = 256;
     resident = per_cu * cus;
-    resident_lds = lds;
+    resident_lds[flat ? 1 : 0] = lds;
   }
   const int64_t units = tiles * (int64_t)((a.n_ticks + a.chunk - 1) / a.chunk);
   const int64_t rounds = (units + resident - 1) / resident;

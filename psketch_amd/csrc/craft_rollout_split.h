@@ -44,11 +44,12 @@ namespace craft {
 // inventory and mask [TILE][32 B] each, pool rows [TILE][CS].
 // (+ the publish outbox: state [TILE] u64, mask [TILE][8] u32)
 __host__ __device__ inline int split_stage_bytes(int tile, int CS) { return tile * (8 + 4 + 64) + tile * CS + tile * 40; }
-__host__ __device__ inline int split_lds_bytes(int tile, int GS, int F, int CS) {
+// (the staging area and the outbox are the continuous pipeline's only: `flat`)
+__host__ __device__ inline int split_lds_bytes(int tile, int GS, int F, int CS, bool flat) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   return up16(3 * tile * GS) + 2 * up16(tile * F) + 2 * tile * kInvStride + 2 * tile * 4 +
          CRAFT_MAX_TASKS * 2 + CRAFT_MAX_RECIPES * 12 + 16 + 32 + 4 * tile * 4 +
-         split_stage_bytes(tile, CS);
+         (flat ? split_stage_bytes(tile, CS) : 0);
 }
 
 // FLAT: the continuous pipeline (one unit per tile, observations on: RolloutArgs.flat);
@@ -651,8 +652,28 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
       const int64_t env0 = (int64_t)t * TILE;
       const int nE = (int)min((int64_t)TILE, n - env0);
 
-      // A: wave 0 takes over the tile (after its previous chunk is published)
+      // Publishing the tile for the unit (t, c + 1) (as craft_rollout.h).  Without observation
+      // ring reuse inside the launch (ring >= n_ticks) only wave 0's state stores are handed
+      // over: they go write-through (sc1) and lane 0 raises the flag after the wave's own
+      // drain; otherwise every wave drains and lane 0 releases at agent scope first, so a
+      // later chunk rewriting the same ring slot from another XCD lands last.
+      const bool state_only = a.ring >= a.n_ticks;
+      const bool handoff = c + 1 < n_chunks;
+      auto full_release = [&]() __attribute__((always_inline)) {   // every wave, the same barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      };
+      // Each role's whole unit sits in its own branch (wave 0: take the tile over, C, publish;
+      // wave 1: D; the rest: E), with the same barriers in the same order, so that wave 0's env
+      // state is not live in the other roles' loops.
       if (tid < 64) {
+        // A: wave 0 takes over the tile (after its previous chunk is published)
         if (c > 0) {
           bool ok = true;
           if (tid == 0) {
@@ -669,56 +690,42 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
           load_tile(t, 0, std::false_type{});
           tick_c(k0, 0, false);                         // C(0) -> buffer 0
         }
-      }
-
-      // the pipeline: interval i runs C(i+1) | D(i) | E(i-1), one barrier each
-      if (!want_obs) {
-        if (tid < TILE)
-          for (int q = 1; q < nq; ++q) tick_c(k0 + q, q, false);
-      } else {
-        __syncthreads();                                // C(0) complete
-        if (tid < 64) {
+        // the pipeline: interval i runs C(i+1) | D(i) | E(i-1), one barrier each
+        if (want_obs) {
+          __syncthreads();                              // C(0) complete
           for (int i = 0; i <= nq; ++i) {
             if (tid < TILE && i + 1 < nq) tick_c(k0 + i + 1, i + 1, false);
             __syncthreads();
           }
-        } else if (tid < 128) {
-          for (int i = 0; i <= nq; ++i) {
-            if (i < nq) scatter_d(i, nE);
-            __syncthreads();
-          }
-        } else {
-          for (int i = 0; i <= nq; ++i) {
-            if (i >= 1) stream_e(i - 1, t, k0 + i - 1, false);
-            __syncthreads();
-          }
+        } else if (tid < TILE) {
+          for (int q = 1; q < nq; ++q) tick_c(k0 + q, q, false);
         }
-      }
-
-      // publish the tile for the unit (t, c + 1) (as craft_rollout.h).  Without observation
-      // ring reuse inside the launch (ring >= n_ticks) only wave 0's state stores are handed
-      // over: they go write-through (sc1) and lane 0 raises the flag after the wave's own
-      // drain; otherwise every wave drains and lane 0 releases at agent scope first, so a
-      // later chunk rewriting the same ring slot from another XCD lands last.
-      const bool state_only = a.ring >= a.n_ticks;
-      const bool handoff = c + 1 < n_chunks;
-      if (tid < TILE && live) publish(nq - 1, handoff && state_only);
-      if (handoff && state_only) {
-        if (tid < 64) {
+        if (tid < TILE && live) publish(nq - 1, handoff && state_only);
+        if (handoff && state_only) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (tid == 0)
             __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+        } else if (handoff) {
+          full_release();
         }
-      } else if (handoff) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store((gu32*)(a.tile_done + t), (uint32_t)(c + 1), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (want_obs) {
+          __syncthreads();                              // C(0) complete
+          if (tid < 128) {
+#pragma unroll 1
+            for (int i = 0; i <= nq; ++i) {
+              if (i < nq) scatter_d(i, nE);
+              __syncthreads();
+            }
+          } else {
+            for (int i = 0; i <= nq; ++i) {
+              if (i >= 1) stream_e(i - 1, t, k0 + i - 1, false);
+              __syncthreads();
+            }
+          }
         }
+        if (handoff && !state_only) full_release();
       }
       __syncthreads();                                  // s_ctrl and the LDS rows are reused
     }

@@ -26,8 +26,11 @@ namespace craft {
 // every env's new state (craft_step_teach), TL lanes per env, while the first
 // kThreads stream the observations: the BFS reads the grid rows the tick left in
 // LDS.  NW = 32-bit words per cell set (teach_env).
+#ifndef CRAFT_TT_WPE
+#define CRAFT_TT_WPE 4
+#endif
 template <int WIN, int MODE, int TILE, int TL = 0, int NW = 0>
-__global__ __launch_bounds__(kThreads + TILE * TL) void tile_kernel(SimView v, TileArgs a) {
+__global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) void tile_kernel(SimView v, TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
   uint8_t* s_grid = smem;
