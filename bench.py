@@ -289,13 +289,17 @@ def run(args):
         D.barrier()
         torch.cuda.synchronize()
 
-    # ---- timed region: exactly args.steps ticks, barrier + synchronize on both sides -------
+    # ---- timed region: exactly args.steps ticks, barrier + synchronize on both sides.  Each
+    # rank's clock stops when its own GPU is done (synchronize), before the closing barrier's
+    # exchange; the line reports the slowest rank. -------------------------------------------
     barrier()
     t0 = time.perf_counter()
     for k in timed_plan:
         launch(k)
-    barrier()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.barrier()
+    elapsed = D.max_over_ranks(t1 - t0, dev)
 
     # ---- per-launch kernel duration, HIP events on the launch stream (outside the timed
     # region): launches of k_eff ticks, as many as the timed region had (at least 8) ----------
