@@ -57,7 +57,7 @@ class RolloutInfo:
 
 
 def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_obs=False,
-               timing=None):
+               timing=None, fused_teacher=True):
     """One rollout of sim.n_envs episodes.
 
     spec: (scenario, x, y, dir, task), each n_envs ints (device or host).
@@ -70,6 +70,9 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
       (student.receive, imitation.py:75-77) with the int32 device tensor.
     timing: optional dict; receives host wall seconds of the setup, the tick
       loop and the distances/summary phases (each ends at a device sync).
+    fused_teacher: when not is_eval, each tick's step also labels the new states
+      (craft_step_teach: the next tick's ref_actions, in the same launch);
+      False runs craft_teacher on a side stream, overlapping the student.
     """
     import time
     t_start = time.perf_counter()
@@ -87,6 +90,7 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     seqs = torch.full((T, n), -1, dtype=torch.int32, device=dev)
     live = torch.zeros(T, dtype=torch.int32, device=dev)     # 1: some env still running after tick t
     ref = torch.empty(n, dtype=torch.int32, device=dev)
+    ref_next = torch.empty(n, dtype=torch.int32, device=dev) if fused_teacher else None
     bc = None
     if not is_eval:
         if behavior_clone is None:
@@ -100,7 +104,7 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     # side stream while the student's act(t) runs on the main stream.
     main = torch.cuda.current_stream(dev)
     side = None
-    if not is_eval:
+    if not is_eval and not fused_teacher:
         side = getattr(sim, "_teacher_stream", None)
         if side is None:                         # created once per simulator (costly)
             side = sim._teacher_stream = torch.cuda.Stream(dev)
@@ -115,7 +119,10 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
         labels_ready.record(side)
 
     if not is_eval:
-        launch_teacher()
+        if fused_teacher:
+            sim.teacher(action_out=ref)          # the initial states' labels; then every step's
+        else:
+            launch_teacher()
     t_loop = time.perf_counter()
     t = 0
     while True:
@@ -123,22 +130,26 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
         if not torch.is_tensor(actions):
             actions = torch.as_tensor(np.asarray(actions), device=dev)
         actions = actions.to(device=dev, dtype=torch.int32).reshape(n)
-        if not is_eval:
+        if not is_eval and not fused_teacher:
             main.wait_event(labels_ready)
         if keep_obs:
             obs = obs_hist[t + 1]
+        fused = not is_eval and fused_teacher
         sim.step(actions, tick=t, autoreset=False, obs=obs, success=success,
                  ref_actions=None if is_eval else ref, behavior_clone=bc,
-                 action_record=seqs[t], any_live=live[t:t + 1])
+                 action_record=seqs[t], any_live=live[t:t + 1],
+                 labels=ref_next if fused else None)
         if not is_eval and receive is not None:
             receive(ref.clone())
         t += 1
-        if not is_eval and t < T:
+        if fused:
+            ref, ref_next = ref_next, ref        # this step's labels are the next tick's ref_actions
+        elif not is_eval and t < T:
             launch_teacher()                     # speculative: all -1 if every env is done
         # every env is done once its timer reaches 0 (imitation.py:42, 62-63)
         if t >= T or int(live[t - 1]) == 0:
             break
-    if not is_eval:
+    if side is not None:
         main.wait_stream(side)
     t_end_loop = time.perf_counter()
     # distances (imitation.py:79-91): failed get tasks, initial grid at the final pose

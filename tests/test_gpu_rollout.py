@@ -21,8 +21,10 @@ def torch_policy(W, bias, device):
 
 
 @pytest.mark.parametrize("case", ["dev8", "w12"])
-@pytest.mark.parametrize("mode", ["train", "eval"])
-def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode):
+@pytest.mark.parametrize("mode,fused", [("train", True), ("train", False), ("eval", True)])
+def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode, fused):
+    """fused: the teacher labels come from each step's launch (craft_step_teach); else from
+    craft_teacher on a side stream."""
     from psketch_amd import CraftSim
     from psketch_amd.rollout import do_rollout
     fx = golden("imitation_rollout.npz")
@@ -34,7 +36,7 @@ def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode):
     received = []
     info = do_rollout(sim, tuple(spec.T), torch_policy(fx[f"{case}_W"], fx[f"{case}_bias"], gpu),
                       mode == "eval", behavior_clone=fx[key + "_bc"],
-                      receive=lambda r: received.append(r.cpu().numpy()))
+                      receive=lambda r: received.append(r.cpu().numpy()), fused_teacher=fused)
     ref = info.to_reference()
     A = fx[key + "_action_seqs"]
     assert ref["action_seqs"] == [[int(a) for a in row if a >= 0] for row in A]

@@ -47,22 +47,25 @@ def main():
         return (x @ Wt).argmax(dim=1).to(torch.int32)
 
     bc = np.random.RandomState(0).binomial(1, 0.5, size=args.envs)
-    for mode in ["train", "eval"]:
+    for mode in ["train", "train_side_stream", "eval"]:
         is_eval = mode == "eval"
-        warm = do_rollout(sim, spec, act, is_eval, behavior_clone=bc)   # warm-up (kernels loaded)
+        fused = mode != "train_side_stream"
+        warm = do_rollout(sim, spec, act, is_eval, behavior_clone=bc, fused_teacher=fused)   # warm-up
         int((warm.n_actions - 1).clamp(min=0).sum())
         torch.cuda.synchronize()
         ticks = steps = 0
         phases = {}
         t0 = time.perf_counter()
         for _ in range(args.reps):
-            info = do_rollout(sim, spec, act, is_eval, behavior_clone=bc, timing=phases)
+            info = do_rollout(sim, spec, act, is_eval, behavior_clone=bc, timing=phases,
+                              fused_teacher=fused)
             ticks += info.ticks
             steps += int((info.n_actions - 1).clamp(min=0).sum())
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         print(json.dumps({
             "mode": mode, "config": "3 (eval)" if is_eval else "5 (teacher, mix 0.5)",
+            "teacher": None if is_eval else ("fused into the step" if fused else "side stream"),
             "world": args.world, "obs_format": args.obs_format, "envs": args.envs, "rollouts": args.reps, "ticks": ticks,
             "ms_per_rollout": 1e3 * dt / args.reps, "us_per_tick": 1e6 * dt / ticks,
             "env_ticks_per_s": args.envs * ticks / dt, "live_env_steps_per_s": steps / dt,
