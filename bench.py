@@ -86,7 +86,7 @@ def parse(argv=None):
     p.add_argument("--tile", type=int, default=0, help="envs per workgroup (0 = default)")
     p.add_argument("--obs-store", type=int, default=-1,
                    help="0 write-back, 1 nontemporal, 2 sc1; -1: the measured best for the path "
-                        "(nontemporal for craft_step, write-back for craft_rollout)")
+                        "(nontemporal for craft_step, write-through (sc1) for craft_rollout)")
     p.add_argument("--ticks-per-launch", type=int, default=32,
                    help="K > 1: craft_rollout runs up to K ticks per launch (the same work per "
                         "tick); 1: one craft_step launch per tick")
@@ -240,7 +240,7 @@ def run(args):
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
-    obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 0)
+    obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 2)
     sim.tune(args.tile, 0, obs_store)
     sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]

@@ -143,8 +143,9 @@ int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capaci
  * setting): envs per workgroup tile (16, 32 or 64; 0 = default for the
  * window), the most tile workgroups that may share a CU (0 = no cap, else
  * 3..32), and the cache policy of the observation stores (0 write-back,
- * 1 nontemporal = default, 2 write-through).  Note: craft_sim_tune(.., 0, 0, 0)
- * selects write-back; pass 1 to keep the default policy. */
+ * 1 nontemporal, 2 write-through) for every entry point.  Until it is called,
+ * the tick kernels store nontemporal and craft_rollout write-through (each the
+ * measured best).  Note: craft_sim_tune(.., 0, 0, 0) selects write-back. */
 int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu,
                    int32_t obs_store);
 
