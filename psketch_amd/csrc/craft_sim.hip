@@ -20,6 +20,8 @@ hipError_t launch_rollout(int win, int tile, int threads, const SimView& v, cons
 hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t st);
 hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
                              hipStream_t st);
+hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
+size_t tick2_lds_bytes(int tl, int GS, int F);
 
 namespace {
 
@@ -245,6 +247,15 @@ void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
   *tile = t;
   *threads = nt;
   *split = (t <= 32 && nt >= 320) ? 1 : 0;
+}
+
+// craft_step_teach runs the two-tile tick kernel (craft_tick2.h) for 3x3 windows at the default
+// tile shape; CRAFT_TICK2_TEACH=0 selects the one-tile kernel instead (diagnostic A/B).  The plain
+// tick stays on the one-tile kernel: the two-tile form measured 2-3 us slower without a teacher
+// (tools/ab_tick2.sh).
+bool use_tick2(const craft_sim* s) {
+  static const int on = getenv("CRAFT_TICK2_TEACH") ? atoi(getenv("CRAFT_TICK2_TEACH")) : 1;
+  return s->cfg.window_width == 3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0 && on != 0;
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
@@ -629,8 +640,21 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   const int rc = step_args(s, x, a);
   if (rc != CRAFT_OK) return rc;
   a.label = label_out;
-  // teacher lanes per env: 4 (default) or 1 (CRAFT_TEACH_LANES=1, diagnostic)
-  static const int tl = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 1) ? 1 : 4;
+  if (use_tick2(s)) {
+    // teacher lanes per env in the two-tile kernel: 2 (default) or 4 (CRAFT_TEACH_LANES=4, diagnostic)
+    static const int tl2 = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 4) ? 4 : 2;
+    hipError_t e = craft::launch_tick2(tl2, (s->view.C + 31) / 32, s->view, a,
+                                       craft::tick2_lds_bytes(tl2, s->view.GS, s->view.F),
+                                       reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
+    return CRAFT_OK;
+  }
+  // teacher lanes per env in the one-tile kernel: 4 (default), or 1 / 2 (CRAFT_TEACH_LANES, diagnostic)
+  static const int tl = [] {
+    const char* e = getenv("CRAFT_TEACH_LANES");
+    const int x = e ? atoi(e) : 4;
+    return (x == 1 || x == 2) ? x : 4;
+  }();
   const int tile = craft::kMaxTileEnvs;
   const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
                      CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16;   // + task | frozen words, task_sub, D sync

@@ -162,6 +162,141 @@ __device__ __forceinline__ Bits<NW> quad_or(const Bits<NW>& a) {
   return r;
 }
 
+// OR over the 2 lanes of a pair (DPP quad_perm [1,0,3,2]).
+__device__ __forceinline__ uint32_t pair_or(uint32_t x) {
+  return x | (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> pair_or(const Bits<NW>& a) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r.w[i] = pair_or(a.w[i]);
+  return r;
+}
+
+// LANES = 2: the two lanes of a pair run one query together, lane pl handling the
+// states entered by actions 2pl and 2pl + 1 (DOWN/UP: cell shifts -1/+1; LEFT/RIGHT:
+// -H/+H).  Each lane's two shifts are by the same amount s in opposite directions, so
+// they are plain funnel shifts by a per-lane amount (no per-lane direction select), and a
+// level costs one pair OR instead of two quad steps: about half the instructions per
+// query of LANES = 4, at the same dependent-chain length.  The same forward, reachability
+// and backward passes as bfs_closest_1; everything that steers control flow is
+// pair-uniform.
+template <int NW>
+__device__ __forceinline__ Bits<NW> bshift_up(const Bits<NW>& a, uint32_t s) {   // p -> p + s
+  Bits<NW> r;
+  r.w[0] = a.w[0] << s;
+#pragma unroll
+  for (int i = 1; i < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i], a.w[i - 1], 32u - s);
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> bshift_dn(const Bits<NW>& a, uint32_t s) {   // p -> p - s
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i + 1 < NW; ++i) r.w[i] = __builtin_amdgcn_alignbit(a.w[i + 1], a.w[i], s);
+  r.w[NW - 1] = a.w[NW - 1] >> s;
+  return r;
+}
+template <int NW>
+__device__ bool bfs_closest_2(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits<NW>& valid,
+                              int H, int p0, int d0, int pl, int& first_action, int& path_len,
+                              bool want_action, bool conn) {
+  const uint32_t s = pl ? (uint32_t)H : 1u;     // lo action 2pl moves by -s, hi action 2pl + 1 by +s
+  const int alo = 2 * pl;
+  const Bits<NW> fr = bandn(valid, occ);
+  const Bits<NW> blk_lo = bshift_up(occ, s), blk_hi = bshift_dn(occ, s);   // blk[p] = occ[p + d]
+  const Bits<NW> fa_lo = bshift_up(tgt, s), fa_hi = bshift_dn(tgt, s);     // fa[p] = tgt[p + d]
+  const int dl0 = d0 == 0 ? -1 : d0 == 1 ? 1 : d0 == 2 ? -H : H;
+  const uint32_t psh = __lane_id() & ~1u;                                  // this pair's lanes in a ballot
+  first_action = -1;
+  path_len = -1;
+  Bits<NW> claimed = bzero<NW>();
+  int L = -1, chosen = -1;
+  {
+    const int f0 = p0 + dl0;               // the start state already faces a target: []
+    if (f0 >= 0 && btest(tgt, f0)) {
+      L = 0;
+      chosen = f0;
+      claimed = bbit<NW>(f0);
+    }
+  }
+  Bits<NW> Vlo = (alo == d0) ? bbit<NW>(p0) : bzero<NW>();
+  Bits<NW> Vhi = (alo + 1 == d0) ? bbit<NW>(p0) : bzero<NW>();
+  Bits<NW> U = bbit<NW>(p0);
+  const bool open = bany(bandn(tgt, claimed));
+  for (int depth = 1; open && L < 0; ++depth) {
+    const Bits<NW> nlo = bandn(bor(band(bshift_dn(U, s), fr), band(U, blk_lo)), Vlo);
+    const Bits<NW> nhi = bandn(bor(band(bshift_up(U, s), fr), band(U, blk_hi)), Vhi);
+    Vlo = bor(Vlo, nlo);
+    Vhi = bor(Vhi, nhi);
+    const Bits<NW> nU = pair_or(bor(nlo, nhi));
+    if (!bany(nU)) break;                  // every reachable state visited
+    uint32_t face = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) face |= (nlo.w[i] & fa_lo.w[i]) | (nhi.w[i] & fa_hi.w[i]);
+    if ((uint32_t)(__ballot(face != 0) >> psh) & 0x3u) {   // some lane of the pair faces a target
+      const Bits<NW> hit = bandn(pair_or(band(bor(bshift_dn(nlo, s), bshift_up(nhi, s)), tgt)), claimed);
+      if (bany(hit)) {
+        claimed = bor(claimed, hit);
+        L = depth;
+        chosen = blowest(hit);
+        break;
+      }
+    }
+    U = nU;
+  }
+  if (L < 0) return true;                  // no target at all, or none reachable: None
+  path_len = L;
+  if (bany(bandn(tgt, claimed)) && conn && btest(fr, p0)) {
+    // connected free cells (see bfs_closest): a target is reachable iff it has a free neighbour
+    claimed = bor(claimed, band(pair_or(bor(bshift_dn(fr, s), bshift_up(fr, s))), tgt));
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  } else if (bany(bandn(tgt, claimed))) {
+    Bits<NW> R = bor(pair_or(bor(Vlo, Vhi)), bbit<NW>(p0));
+    for (;;) {
+      const Bits<NW> adj = pair_or(bor(bshift_dn(R, s), bshift_up(R, s)));   // cells next to R
+      claimed = bor(claimed, band(adj, tgt));
+      if (!bany(bandn(tgt, claimed))) break;
+      const Bits<NW> grow = bandn(band(adj, fr), R);
+      if (!bany(grow)) break;
+      R = bor(R, grow);
+    }
+    const Bits<NW> unreached = bandn(tgt, claimed);
+    if (bany(unreached) && blowest(claimed) < bhighest(unreached)) return false;
+  }
+  if (L == 0 || !want_action) return true;
+  // reverse BFS from the states facing `chosen` (direction a stands at chosen - d_a)
+  Bits<NW> Glo, Ghi;
+  {
+    const int qlo = chosen + (int)s, qhi = chosen - (int)s;
+    Glo = band(bbit<NW>(qlo), fr);
+    Ghi = (qhi >= 0) ? band(bbit<NW>(qhi), fr) : bzero<NW>();
+    Vlo = Glo;
+    Vhi = Ghi;
+  }
+  for (int k = 1; k < L; ++k) {
+    // predecessors, any direction: moved here (from p - d) or turned in place (blocked)
+    const Bits<NW> P = pair_or(bor(bor(band(bshift_up(Glo, s), fr), band(Glo, blk_lo)),
+                                   bor(band(bshift_dn(Ghi, s), fr), band(Ghi, blk_hi))));
+    Glo = bandn(P, Vlo);
+    Ghi = bandn(P, Vhi);
+    Vlo = bor(Vlo, Glo);
+    Vhi = bor(Vhi, Ghi);
+  }
+  // the smallest action whose level-1 state lies within reverse distance L-1
+  const int qlo0 = p0 - (int)s, qhi0 = p0 + (int)s;
+  const int qlo = btest(fr, qlo0) ? qlo0 : p0, qhi = btest(fr, qhi0) ? qhi0 : p0;
+  const bool ok_lo = !(qlo == p0 && alo == d0) && btest(Vlo, qlo);
+  const bool ok_hi = !(qhi == p0 && alo + 1 == d0) && btest(Vhi, qhi);
+  const uint32_t blo = (uint32_t)(__ballot(ok_lo) >> psh) & 0x3u, bhi = (uint32_t)(__ballot(ok_hi) >> psh) & 0x3u;
+  // actions 0, 1 (lane 0 of the pair) and 2, 3 (lane 1)
+  const uint32_t acts = (blo & 1u) | ((bhi & 1u) << 1) | ((blo >> 1) << 2) | ((bhi >> 1) << 3);
+  first_action = acts ? __ffs(acts) - 1 : -1;
+  return true;
+}
+
 // LANES = 4: the four lanes of a quad run one query together, lane ql handling the states
 // entered by action ql (its direction's visited set and blocked mask): each
 // level is then one action's worth of bitset work plus two quad ORs, instead of
@@ -173,6 +308,8 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
                             bool want_action, bool conn) {
   if (LANES == 1)
     return bfs_closest_1<NW>(occ, tgt, valid, H, p0, d0, first_action, path_len, want_action, conn);
+  if (LANES == 2)
+    return bfs_closest_2<NW>(occ, tgt, valid, H, p0, d0, ql, first_action, path_len, want_action, conn);
   const int dla = ql == 0 ? -1 : ql == 1 ? 1 : ql == 2 ? -H : H;   // this lane's action
   const Bits<NW> fr = bandn(valid, occ);
   const Bits<NW> blk = bshift_var(occ, -dla);                         // blk[p] = occ[p + dla]
@@ -275,11 +412,18 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t x, int s) {
 }
 
 
+// Lane s of the pair's value, in both lanes of the pair (DPP quad_perm [s,s,2+s,2+s]).
+__device__ __forceinline__ uint32_t pair_bcast(uint32_t x, int s) {
+  return s == 0 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false)
+                : (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);
+}
+
 // Occupancy and `kind` target sets of a grid row (kind ids, 4 cells per 32-bit word
 // of row32, nq words) minus the cells set in m: SWAR byte tests on whole words
 // (nonzero byte: ((w & 0x7f..) + 0x7f..) | w has bit 7 set; equal byte: the same on
 // w ^ kind), 32 cells per result word, no per-cell work.  With LANES = 4 the quad
-// splits the words (lane ql builds words ql, ql + 4, ...) and broadcasts them.
+// splits the words (lane ql builds words ql, ql + 4, ...) and broadcasts them; LANES = 2
+// likewise over a pair.
 template <int NW, int LANES>
 __device__ __forceinline__ void grid_bits(const uint32_t* row32, int nq, const uint32_t (&m)[8],
                                           uint32_t kind, int ql, const Bits<NW>& valid,
@@ -308,8 +452,10 @@ __device__ __forceinline__ void grid_bits(const uint32_t* row32, int nq, const u
   }
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
-    const uint32_t oi = LANES == 1 ? po[i / LANES] : quad_bcast(po[i / LANES], i % LANES);
-    const uint32_t ti = LANES == 1 ? pt[i / LANES] : quad_bcast(pt[i / LANES], i % LANES);
+    const uint32_t oi = LANES == 1 ? po[i / LANES]
+                      : LANES == 2 ? pair_bcast(po[i / LANES], i % LANES) : quad_bcast(po[i / LANES], i % LANES);
+    const uint32_t ti = LANES == 1 ? pt[i / LANES]
+                      : LANES == 2 ? pair_bcast(pt[i / LANES], i % LANES) : quad_bcast(pt[i / LANES], i % LANES);
     occ.w[i] = oi & valid.w[i];
     tgt.w[i] = ti & oi & valid.w[i];
   }

@@ -2,13 +2,16 @@
 // (craft_teacher): one lane or one quad of lanes per item, each env's grid
 // rebuilt from its pool row and cleared-cell mask; the per-env body is
 // teach_env (craft_teach.h).
+#include <cstdlib>
+
 #include "craft_teach.h"
 
 namespace craft {
 
-// Batches up to this many items run 4 lanes per item (tools/teacher_bench.py:
-// latency-bound below it, throughput-bound above).
-constexpr int64_t kTeacherQuadMaxItems = 32768;
+// Batches up to this many items run 4 lanes per item, larger ones 2 (tools/ab_teach_lanes.sh,
+// profiles/r02/teach_lanes: 4096 items 12.1 / 15.9 / 25.5 us with 4 / 2 / 1 lanes, 32768
+// items 16.2 / 15.0 / 22.9, 65536 items 21.7 / 19.8 / 24.4).
+constexpr int64_t kTeacherQuadMaxItems = 8192;
 
 struct TeachArgs {
   const int32_t* slots;
@@ -18,10 +21,11 @@ struct TeachArgs {
   int32_t* len_out;
 };
 
-// DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30), one lane per slot.
-// LANES lanes per item: 4 (quad-parallel BFS) shortens each query's dependent
-// chain, which is what bounds a small batch; 1 does the least total work, which is
-// what bounds a large one (launch_teacher picks by batch size).
+// DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30), LANES lanes per item:
+// 4 (quad-parallel BFS) gives each query the shortest dependent chain, which is what
+// bounds a small batch; 2 (a pair, one shift amount per lane) does about half the
+// instructions per query at nearly the same chain length, which is what bounds a large
+// one; 1 does the least work but the longest chain (launch_teacher picks by batch size).
 template <int NW, int LANES>
 __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   // the task tables in LDS: the hint-tree walk reads them in a dependent chain
@@ -33,7 +37,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   }
   __syncthreads();
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
-  const int ql = LANES == 4 ? (threadIdx.x & 3) : 0;
+  const int ql = (int)(threadIdx.x % LANES);
   if (i >= a.n) return;                  // lane-group-uniform: a group never straddles two items
   const bool lead = ql == 0;             // the lane that writes the outputs and latches errors
   const int64_t slot = a.slots ? (int64_t)a.slots[i] : i;
@@ -95,12 +99,18 @@ hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const 
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
   TeachArgs a{slots, tasks, n, act_out, len_out};
   // nw = 32-bit words per cell set: 8x8 -> 2, 10x10 -> 4, 12x12 -> 5, 16x16 -> 8
-  const bool quad = n <= kTeacherQuadMaxItems;
-  const unsigned blocks = (unsigned)(((quad ? 4 : 1) * n + 255) / 256);
-#define CRAFT_TEACH(NWV)                                                                           \
-  do {                                                                                             \
-    if (quad) hipLaunchKernelGGL((teacher_kernel<NWV, 4>), dim3(blocks), dim3(256), 0, st, v, a);  \
-    else hipLaunchKernelGGL((teacher_kernel<NWV, 1>), dim3(blocks), dim3(256), 0, st, v, a);       \
+  static const int forced = [] {                  // CRAFT_TEACHER_LANES=1/2/4: diagnostic override
+    const char* e = getenv("CRAFT_TEACHER_LANES");
+    const int x = e ? atoi(e) : 0;
+    return (x == 1 || x == 2 || x == 4) ? x : 0;
+  }();
+  const int lanes = forced ? forced : (n <= kTeacherQuadMaxItems ? 4 : 2);
+  const unsigned blocks = (unsigned)((lanes * n + 255) / 256);
+#define CRAFT_TEACH(NWV)                                                                               \
+  do {                                                                                                 \
+    if (lanes == 4) hipLaunchKernelGGL((teacher_kernel<NWV, 4>), dim3(blocks), dim3(256), 0, st, v, a); \
+    else if (lanes == 2) hipLaunchKernelGGL((teacher_kernel<NWV, 2>), dim3(blocks), dim3(256), 0, st, v, a); \
+    else hipLaunchKernelGGL((teacher_kernel<NWV, 1>), dim3(blocks), dim3(256), 0, st, v, a);           \
   } while (0)
   if (nw <= 2) CRAFT_TEACH(2);
   else if (nw <= 4) CRAFT_TEACH(4);

@@ -3,7 +3,9 @@
 // tick).  The tile kernel (craft_tile.h) with TILE * TL teacher threads beside
 // its 256: the tick's waves stream the observations while the teacher waves run
 // teach_env on the grid rows the tick left in LDS, so the teacher reads no grid
-// from HBM and needs no launch of its own.
+// from HBM and needs no launch of its own.  For 3x3 windows the two-tile tick
+// kernel (craft_tick2.h) serves craft_step_teach.
+#include "craft_tick2.h"
 #include "craft_tile.h"
 
 namespace craft {
@@ -36,10 +38,45 @@ static hipError_t launch_tt_nw(int nw, int win, const SimView& v, const TileArgs
   return launch_tt_win<TL, 8>(win, v, a, lds, st);
 }
 
-// tl = teacher lanes per env: 4 (a quad per env, 4 teacher waves) or 1 (one wave).
+// tl = teacher lanes per env: 2 (a pair per env, 2 teacher waves), 4 (a quad, 4 waves) or
+// 1 (one wave).
 hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
                              hipStream_t st) {
-  return tl == 1 ? launch_tt_nw<1>(nw, win, v, a, lds, st) : launch_tt_nw<4>(nw, win, v, a, lds, st);
+  if (tl == 1) return launch_tt_nw<1>(nw, win, v, a, lds, st);
+  if (tl == 4) return launch_tt_nw<4>(nw, win, v, a, lds, st);
+  return launch_tt_nw<2>(nw, win, v, a, lds, st);
+}
+
+// The two-tile tick kernel (craft_tick2.h) for craft_step_teach, 3x3 windows: 2 or 4 teacher
+// lanes per env, 4 tick waves (8 would leave the BFS too few registers at 2 workgroups per CU).
+constexpr int kTick2Tiles = 2, kTick2TickWaves = 4;
+
+size_t tick2_lds_bytes(int /*tl*/, int GS, int F) {
+  return (size_t)tick2_lds(kTick2Tiles, kTick2TickWaves, GS, F).bytes;
+}
+
+template <int TL, int NW>
+static hipError_t launch_t2(const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+  constexpr int TW = kTick2TickWaves;
+  const int64_t per = (int64_t)kTick2Tiles * kTick2Tile;
+  const int64_t blocks = (a.n + per - 1) / per;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((tick2_kernel<3, kTick2Tiles, TW, TL, NW>), dim3((unsigned)blocks),
+                     dim3(64 * TW + kTick2Tiles * kTick2Tile * TL), lds, st, v, a);
+  return hipGetLastError();
+}
+
+template <int TL>
+static hipError_t launch_t2_nw(int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+  if (nw <= 2) return launch_t2<TL, 2>(v, a, lds, st);
+  if (nw <= 4) return launch_t2<TL, 4>(v, a, lds, st);
+  if (nw <= 5) return launch_t2<TL, 5>(v, a, lds, st);
+  return launch_t2<TL, 8>(v, a, lds, st);
+}
+
+hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+  if (tl == 4) return launch_t2_nw<4>(nw, v, a, lds, st);
+  return launch_t2_nw<2>(nw, v, a, lds, st);
 }
 
 }  // namespace craft
