@@ -302,18 +302,18 @@ def run(args):
     elapsed = D.max_over_ranks(t1 - t0, dev)
 
     # ---- per-launch kernel duration, HIP events on the launch stream (outside the timed
-    # region): launches of k_eff ticks, as many as the timed region had (at least 8) ----------
+    # region): m back-to-back launches of k_eff ticks (as many as the timed region had, at
+    # least 8) between one pair of events, so no event sits between two launches -------------
     kstream = torch.cuda.current_stream(dev)
     m = min(max(len(timed_plan), 8), 200)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(m)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    for a, b in evs:
-        a.record(kstream)
+    ev0.record(kstream)
+    for _ in range(m):
         launch(k_eff)
-        b.record(kstream)
+    ev1.record(kstream)
     torch.cuda.synchronize()
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))     # per launch (k_eff ticks)
+    kernel_ms = ev0.elapsed_time(ev1) / m                                # per launch (k_eff ticks)
 
     # ---- scalar episode summary: one RCCL all-reduce of int64[3] ----------------------------
     stats = D.reduce_episode_stats(sim.stats()).cpu().tolist()

@@ -142,6 +142,9 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   int32_t chunk;           // ticks per work unit
   unsigned long long* queue;   // work-unit counter: unit = the value fetched - qbase
   unsigned long long qbase;    // the counter's value at the launch (kept by the host)
+  // split kernel, per-unit path: workgroup b takes unit b without a claim, later units come
+  // from queue[1] (its value at the launch: qbase1); a launch adds max(units, grid) to it
+  unsigned long long qbase1;
   int64_t* grid_out;       // host side only: the launch reports its grid size here
   uint32_t* tile_done;     // per tile: chunks completed in this launch, zeroed before the launch
   int32_t flat;            // split kernel, one unit per tile: one continuous pipeline (no queue)

@@ -640,11 +640,29 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   } else {
     (void)s_out;
     (void)s_stage;
-    // ---- work units (tile t, chunk c) from the queue, one pipeline fill and drain each --------
+#ifdef CRAFT_STAMPS
+    // diagnostic build only: s_memrealtime (10 ns) per workgroup -> stamps[block][16]: 0 start,
+    // 1 + i the claim of its unit i (i < 12), 13 its first unit's first stores issued, 14 units
+    // done, 15 end
+    uint64_t* srow_t = v.stamps ? v.stamps + 16 * (int64_t)blockIdx.x : nullptr;
+    if (tid == 0 && srow_t) srow_t[0] = __builtin_amdgcn_s_memrealtime();
+    int n_done = 0;
+#endif
+    // ---- work units (tile t, chunk c), one pipeline fill and drain each: unit b first (no
+    // claim: 512 claims of one counter at the launch's start took up to ~8 us to return),
+    // then units gridDim.x + (claims of queue[1]); every workgroup ends with one claim past
+    // the last unit, so a launch adds max(units, grid) to queue[1] -------------------------------
+    bool first = (uint32_t)blockIdx.x < n_units;
     for (;;) {
-      if (tid == 0) s_ctrl[0] = (uint32_t)(atomicAdd(a.queue, 1ull) - a.qbase);
+      if (tid == 0)
+        s_ctrl[0] = first ? (uint32_t)blockIdx.x
+                          : (uint32_t)(gridDim.x + (atomicAdd(a.queue + 1, 1ull) - a.qbase1));
+      first = false;
       __syncthreads();                                  // also: s_task / rows ready
       const uint32_t u = s_ctrl[0];
+#ifdef CRAFT_STAMPS
+      if (tid == 0 && srow_t && n_done < 12) srow_t[1 + n_done] = __builtin_amdgcn_s_memrealtime();
+#endif
       if (u >= n_units) break;                          // workgroup-uniform exit
       const int t = (int)(u % (uint32_t)n_tiles), c = (int)(u / (uint32_t)n_tiles);
       const int k0 = c * a.chunk, k1 = min(a.n_ticks, k0 + a.chunk);
@@ -721,6 +739,9 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
           } else {
             for (int i = 0; i <= nq; ++i) {
               if (i >= 1) stream_e(i - 1, t, k0 + i - 1, false);
+#ifdef CRAFT_STAMPS
+              if (tid == 128 && srow_t && n_done == 0 && i == 1) srow_t[13] = __builtin_amdgcn_s_memrealtime();
+#endif
               __syncthreads();
             }
           }
@@ -728,7 +749,16 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
         if (handoff && !state_only) full_release();
       }
       __syncthreads();                                  // s_ctrl and the LDS rows are reused
+#ifdef CRAFT_STAMPS
+      ++n_done;
+#endif
     }
+#ifdef CRAFT_STAMPS
+    if (tid == 0 && srow_t) {
+      srow_t[14] = (uint64_t)n_done;
+      srow_t[15] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
   }
 
   if (tid == 0) {

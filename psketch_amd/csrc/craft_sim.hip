@@ -2,6 +2,7 @@
 // scenario pool, launches, state I/O and episode statistics.
 // Kernels: craft_tile.hip (tick / transition / observe / reset), craft_rollout.hip
 // (multi-tick), craft_teacher.hip, craft_scenarios.hip (pool generation).
+#include <algorithm>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -151,6 +152,7 @@ struct craft_sim {
   bool sync_zeroed = false;         // d_sync zeroed once; then the counter only grows
   int rollout_obs_policy = 2;       // craft_rollout's observation stores until craft_sim_tune sets one:
                                     // write-through, 1.5 % faster than write-back (tools/ab_store.sh)
+  uint64_t queue1_next = 0;         // queue[1] (the split kernel's per-unit path) at the next launch
   uint64_t queue_next = 0;          // the counter's value at the next launch (every launch adds
                                     // its units + its grid: one fetch past the end per workgroup)
   std::string last_error;
@@ -711,8 +713,10 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
     HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
     s->sync_zeroed = true;
     s->queue_next = 0;
+    s->queue1_next = 0;
   }
   a.qbase = s->queue_next;
+  a.qbase1 = s->queue1_next;
   int64_t grid = 0;
   a.grid_out = &grid;
   SimView view = s->view;
@@ -720,7 +724,10 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, view, a, lds_bytes(s, tile, 2, true),
                                        reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");
-  if (grid > 0) s->queue_next += (uint64_t)(units + grid);
+  // the split kernel's per-unit path counts on queue[1] (craft_rollout_split.h), the others on
+  // queue[0]
+  if (grid > 0 && split && !flat) s->queue1_next += (uint64_t)std::max<int64_t>(units, grid);
+  else if (grid > 0) s->queue_next += (uint64_t)(units + grid);
   return CRAFT_OK;
 }
 
