@@ -337,9 +337,10 @@ def run(args):
             kname = f"tile_kernel<{win}, MODE_TICK, {tile}>"
             if teacher and args.teacher_mode == "fused":
                 nw = (sim.width * sim.height + 31) // 32
-                # craft_sim.hip use_tick2: the two-tile kernel for 3x3 windows at the default tile
+                # craft_sim.hip use_tick2: the two-tile kernel for 3x3 windows at the default
+                # tile from 32768 envs
                 kname = (f"tick2_kernel<3, 2, 4, 2, {nw}> (craft_step_teach)"
-                         if win == 3 and tile == 64 and os.environ.get("CRAFT_TICK2_TEACH", "1") != "0"
+                         if win == 3 and tile == 64 and n >= 32768
                          else f"tile_kernel<{win}, MODE_TICK, 64, 4, {nw}> (craft_step_teach)")
             elif teacher:
                 kname += " + teacher_kernel"

@@ -166,6 +166,13 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * for 3x3 windows, else the handle's tile with 256 threads (512 for 64-env tiles). */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
+/* Which kernel craft_step_teach launches: 0 (default) = the measured best (the two-tile
+ * kernel with 2 teacher lanes per env for 3x3 windows at >= 32768 envs, else the one-tile
+ * kernel with 4), 1 = the one-tile kernel, 2 = the two-tile kernel (3x3 windows and the
+ * default tile only; otherwise the one-tile kernel).  Results are identical for every
+ * setting.  Replaces nothing in the reference (a tuning knob, like craft_sim_tune). */
+int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel);
+
 /* The launch shape the next craft_rollout will use, resolved from the knobs above:
  * envs per tile workgroup, threads per workgroup, and split = 1 for the
  * split-producer kernel (rollout_split_kernel), 0 for rollout_kernel.  Lets a

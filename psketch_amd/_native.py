@@ -112,6 +112,7 @@ SIGNATURES = {
     "craft_sim_tune": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),
+    "craft_sim_tune_teach": (_i32, [_vp, _i32]),
     "craft_sim_rollout_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                        ctypes.POINTER(_i32)]),
     "craft_sim_tile_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),

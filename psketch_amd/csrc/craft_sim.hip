@@ -152,6 +152,7 @@ struct craft_sim {
   bool sync_zeroed = false;         // d_sync zeroed once; then the counter only grows
   int rollout_obs_policy = 2;       // craft_rollout's observation stores until craft_sim_tune sets one:
                                     // write-through, 1.5 % faster than write-back (tools/ab_store.sh)
+  int teach_kernel = 0;             // craft_sim_tune_teach: 0 auto, 1 one-tile, 2 two-tile
   uint64_t queue1_next = 0;         // queue[1] (the split kernel's per-unit path) at the next launch
   uint64_t queue_next = 0;          // the counter's value at the next launch (every launch adds
                                     // its units + its grid: one fetch past the end per workgroup)
@@ -252,12 +253,14 @@ void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
 }
 
 // craft_step_teach runs the two-tile tick kernel (craft_tick2.h) for 3x3 windows at the default
-// tile shape; CRAFT_TICK2_TEACH=0 selects the one-tile kernel instead (diagnostic A/B).  The plain
-// tick stays on the one-tile kernel: the two-tile form measured 2-3 us slower without a teacher
-// (tools/ab_tick2.sh).
+// tile shape from 32768 envs (tools/teacher_bench.py: 30.2 vs 38.1 us at 65536, level at 32768,
+// 19.4 vs 16.7 us at 4096, where its 128-env workgroups leave the chip a third full);
+// craft_sim_tune_teach forces either kernel.  The plain tick stays on the one-tile kernel: the
+// two-tile form measured 2-3 us slower without a teacher (tools/ab_tick2.sh).
 bool use_tick2(const craft_sim* s) {
-  static const int on = getenv("CRAFT_TICK2_TEACH") ? atoi(getenv("CRAFT_TICK2_TEACH")) : 1;
-  return s->cfg.window_width == 3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0 && on != 0;
+  if (s->cfg.window_width != 3 || s->tile != craft::kMaxTileEnvs || s->resident_cap != 0) return false;
+  if (s->teach_kernel) return s->teach_kernel == 2;
+  return s->n_envs >= 32768;
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
@@ -409,6 +412,14 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
   s->resident_cap = max_resident_per_cu;
   s->view.obs_policy = obs_store;
   s->rollout_obs_policy = obs_store;
+  return CRAFT_OK;
+}
+
+int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel) {
+  if (!s) return CRAFT_EINVAL;
+  if (kernel < 0 || kernel > 2)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile) or 2 (two-tile)");
+  s->teach_kernel = kernel;
   return CRAFT_OK;
 }
 

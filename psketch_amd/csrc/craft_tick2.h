@@ -25,7 +25,7 @@
 // a teacher (TL = 0) the same structure measured 2-3 us slower than the one-tile kernel
 // (half the streaming waves per CU), so craft_step keeps that one.
 // Results are identical to tile_kernel<WIN, MODE_TICK> + the teacher: the same tests run
-// both (CRAFT_TICK2_TEACH=0 selects the one-tile kernel).
+// both (craft_sim_tune_teach selects either kernel).
 #pragma once
 #include "craft_obs.h"
 #include "craft_teach.h"

@@ -89,6 +89,12 @@ class CraftSim:
         self._check(N.lib().craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
                     "craft_sim_tune_rollout")
 
+    def tune_teach(self, kernel=0):
+        """Which kernel step(..., labels=) launches (craft_sim_tune_teach): 0 the
+        measured best, 1 the one-tile kernel, 2 the two-tile kernel (3x3 windows);
+        results are identical for every setting."""
+        self._check(N.lib().craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
+
     def rollout_shape(self):
         """(tile_envs, threads, split) the next rollout() launches with, as the
         library resolves its knobs (craft_sim_rollout_shape)."""

@@ -14,22 +14,24 @@ from tests.test_gpu_parity import host, sim_with_pool
 pytestmark = pytest.mark.gpu
 
 
-# 3x3 windows at the default tile shape run the two-tile kernel (craft_tick2.h); other windows
-# and tuned tile shapes the one-tile kernel (craft_tile.h)
-@pytest.mark.parametrize("world,W,n,T,autoreset,given,tile", [
+# kernel: 0 the library's choice (the two-tile kernel, craft_tick2.h, for 3x3 windows from
+# 32768 envs), 1 the one-tile kernel (craft_tile.h), 2 the two-tile kernel (3x3 windows only)
+@pytest.mark.parametrize("world,W,n,T,autoreset,given,kernel", [
     ("craft_medium_12x12", 12, 65536, 45, True, False, 0),  # config 5's size, across episode ends
-    ("craft_medium_12x12", 12, 5000, 45, False, True, 0),   # frozen envs (label -1), a partial tile
-    ("craft_medium_12x12", 12, 4000, 30, True, True, 32),   # the one-tile kernel, 3x3 window
-    ("craft_medium", 8, 3000, 30, True, True, 0),           # 8x8: two words per cell set
-    ("craft_medium_12x12_w5", 12, 2048, 20, True, False, 0),
-    ("craft_large", 10, 1024, 20, True, False, 0)])         # 10x10: four words per cell set
-def test_step_teach_equals_step_then_teacher(world, W, n, T, autoreset, given, tile):
+    ("craft_medium_12x12", 12, 5000, 45, False, True, 2),   # frozen envs (label -1), a partial tile
+    ("craft_medium_12x12", 12, 5000, 45, False, True, 1),
+    ("craft_medium_12x12", 12, 4000, 30, True, True, 0),
+    ("craft_medium", 8, 3000, 30, True, True, 2),           # 8x8: two words per cell set
+    ("craft_medium", 8, 3000, 30, True, True, 1),
+    ("craft_medium_12x12_w5", 12, 2048, 20, True, False, 2),  # w = 5: always the one-tile kernel
+    ("craft_large", 10, 1024, 20, True, False, 2),          # 10x10: four words per cell set
+    ("craft_large", 10, 1024, 20, True, False, 1)])
+def test_step_teach_equals_step_then_teacher(world, W, n, T, autoreset, given, kernel):
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 256)
     specs = synthetic_specs(pool, W, W, n, 0, seed=6, task_ids=[t.id for t in tm.dataset_tasks()])
     a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
-    if tile:
-        a.tune(tile, 0, 1)
+    a.tune_teach(kernel)
     a.reset(*specs)
     b.reset(*specs)
     F = a.n_features

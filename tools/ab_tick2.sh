@@ -11,7 +11,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc
 fi
 for rep in 1 2; do
-  for cfg in "tick2" "tick2_tl4:CRAFT_TEACH_LANES=4" "one_tile:CRAFT_TICK2_TEACH=0"; do
+  for cfg in "tick2:TEACH_KERNEL=2" "tick2_tl4:TEACH_KERNEL=2,CRAFT_TEACH_LANES=4" "one_tile:TEACH_KERNEL=1"; do
     name=${cfg%%:*}; envs=""; [ "$name" != "$cfg" ] && envs=${cfg#*:}
     env ${envs//,/ } TEACHER_ENVS=${TEACHER_ENVS:-65536} timeout -k 10 200 python tools/teacher_bench.py > "$OUT/$name.$rep.json" 2> "$OUT/$name.$rep.err"
     rc=$?; [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -3 "$OUT/$name.$rep.err"; exit $rc; }

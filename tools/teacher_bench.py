@@ -20,6 +20,7 @@ for world, n in [(w, n) for w in (sys.argv[1:] or ["craft_medium_12x12"]) for n 
     sim = CraftSim(world, n_envs=n, device=0, pool_capacity=1024)
     g, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, 1024)
     sim.load_pool(g)
+    sim.tune_teach(int(os.environ.get("TEACH_KERNEL", "0")))   # craft_step_teach's kernel (0 = auto)
     sim.reset(*synthetic_specs(g, sim.width, sim.height, n, 0, 0, [t.id for t in sim.task_manager.dataset_tasks()]))
     obs = sim.empty_obs()
     act = torch.empty(n, dtype=torch.int32, device="cuda")
