@@ -44,15 +44,16 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def bytes_per_env_step(W, H, window, F, teacher=False):
+def bytes_per_env_step(W, H, window, F, teacher=False, obs_bytes=4):
     """Algorithmic HBM bytes per env-step: 57 B of step state
     (action 1 + agent state r/w 48 + facing/target cells 2 + cell write 1 +
     reward 4 + done 1) + the fp32 observation row F*4 + the pooled window's
     grid cells min(w^2, W) * min(w^2, H); the teacher adds the W*H navigation
     grid + the 2 B task id, and its 4 B label ("C5 adds the
-    teacher reads")."""
+    teacher reads").  obs_bytes: bytes per observation element (4 fp32, 2 bf16,
+    1 u8: the same exact values, craft_sim_set_obs_format)."""
     ww = window * window
-    b = 57 + 4 * F + min(ww, W) * min(ww, H)
+    b = 57 + obs_bytes * F + min(ww, W) * min(ww, H)
     if teacher:
         b += W * H + 2 + 4
     return b
@@ -105,6 +106,9 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=8.0,
                    help="wall seconds of each cpu_baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--obs-format", choices=("f32", "bf16", "u8"), default="f32",
+                   help="observation element type (the same exact values in each; the metric's "
+                        "line is f32, what students/imitation.py:73 feeds the model)")
     p.add_argument("--traffic", default=None,
                    help="PMC traffic JSON (tools/pmc_summary.py); default profiles/pmc_traffic*.json")
     args = p.parse_args(argv)
@@ -242,6 +246,7 @@ def run(args):
     sim.load_pool(grids)
     obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 2)
     sim.tune(args.tile, 0, obs_store)
+    sim.set_obs_format(args.obs_format)
     sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
     specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
@@ -323,7 +328,9 @@ def run(args):
         win = sim.params["WINDOW_WIDTH"]
         total_steps = n * world_size * args.steps
         value = total_steps / elapsed
-        bps = bytes_per_env_step(sim.width, sim.height, win, F, teacher)
+        obs_bytes = {"f32": 4, "bf16": 2, "u8": 1}[sim.obs_format]
+        bps = bytes_per_env_step(sim.width, sim.height, win, F, teacher, obs_bytes)
+        obs_dtype = {"f32": "fp32", "bf16": "bf16", "u8": "u8"}[sim.obs_format]
         if K > 1:
             tile, threads, split = sim.rollout_shape()          # what the library launched
             fmt = {"f32": "0", "bf16": "1", "u8": "2"}[sim.obs_format]
@@ -350,6 +357,8 @@ def run(args):
             "teacher_labels_full_features" if teacher else "random_rollout_full_features")
         if K > 1:
             workload += f"_K{K}"
+        if sim.obs_format != "f32":
+            workload += f"_obs_{sim.obs_format}"
         if teacher:
             workload += "_" + args.teacher_mode
         traffic = None
@@ -375,12 +384,12 @@ def run(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": obs_dtype,
             "data": "synthetic: 1024 make_data.sample_scenario worlds (RandomState(123)), "
                     "per-env init keyed by global id, splitmix64 actions",
             "config": dict({"workload": workload, "world": args.world, "envs_per_gpu": n,
                             "global_batch": n * world_size, "window": win,
-                            "n_features": F, "obs_dtype": "fp32",
+                            "n_features": F, "obs_dtype": obs_dtype,
                             "state_dtype": "u8 (exact small integers; the reference's float64 "
                                            "arrays hold the same values)",
                             "obs_ring": args.ring, "pool": args.pool,

@@ -77,3 +77,13 @@ def test_bytes_per_env_step():
     assert bench.bytes_per_env_step(12, 12, 3, 404) == 1754
     assert bench.bytes_per_env_step(12, 12, 5, 1076) == 4505
     assert bench.bytes_per_env_step(12, 12, 3, 404, teacher=True) == 1754 + 150
+    # bf16 / u8 observations (same values): the observation row shrinks to 2F / F bytes
+    assert bench.bytes_per_env_step(12, 12, 3, 404, obs_bytes=2) == 1754 - 2 * 404
+    assert bench.bytes_per_env_step(12, 12, 3, 404, obs_bytes=1) == 1754 - 3 * 404
+
+
+def test_obs_format_argument():
+    assert bench.parse([]).obs_format == "f32"
+    assert bench.parse(["--obs-format", "u8"]).obs_format == "u8"
+    with pytest.raises(SystemExit):
+        bench.parse(["--obs-format", "f16"])
