@@ -246,7 +246,10 @@ void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
     t = 32;
     nt = 512;
   }
-  if (nt == 0) nt = (t == 64) ? 512 : 256;   // launch_rollout_win's defaults
+  // what launch_rollout_win (craft_rollout.h) instantiates for (t, nt): 64-env tiles run 256
+  // or 512 threads, smaller tiles 128, the split kernel at 320 / 384 / 512, else 256
+  if (t == 64) nt = (nt == 256) ? 256 : 512;
+  else if (nt != 128 && nt != 320 && nt != 384 && nt != 512) nt = 256;
   *tile = t;
   *threads = nt;
   *split = (t <= 32 && nt >= 320) ? 1 : 0;

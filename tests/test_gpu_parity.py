@@ -563,3 +563,24 @@ def test_rollout_fast_path_revalidates_resized_rings():
     with pytest.raises(ValueError):
         sim.rollout(3, tick0=6, obs=ring, done=done)
     sim.check()
+
+
+def test_rollout_shape_reports_the_launched_kernel():
+    """craft_sim_rollout_shape names what craft_rollout launches: the 3x3 default is the split
+    kernel on 32-env tiles x 512 threads; 64-env tiles run 256 or 512 threads (a request for
+    384 runs, and is reported as, 512); smaller tiles run 128, 256 or the split kernel at
+    320 / 384 / 512."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 16)
+    sim = sim_with_pool(world, 256, pool)
+    assert sim.rollout_shape() == (32, 512, True)
+    sim.tune(64, 0, 2)
+    for req, want in ((256, (64, 256, False)), (384, (64, 512, False)), (512, (64, 512, False))):
+        sim.tune_rollout(0, req)
+        assert sim.rollout_shape() == want, req
+    sim.tune(32, 0, 2)
+    for req, want in ((128, (32, 128, False)), (256, (32, 256, False)), (320, (32, 320, True)),
+                      (384, (32, 384, True))):
+        sim.tune_rollout(0, req)
+        assert sim.rollout_shape() == want, req
