@@ -166,12 +166,33 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * for 3x3 windows, else the handle's tile with 256 threads (512 for 64-env tiles). */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
-/* Which kernel craft_step_teach launches: 0 (default) = the measured best (the two-tile
- * kernel with 2 teacher lanes per env for 3x3 windows at >= 32768 envs, else the one-tile
- * kernel with 4), 1 = the one-tile kernel, 2 = the two-tile kernel (3x3 windows and the
- * default tile only; otherwise the one-tile kernel).  Results are identical for every
- * setting.  Replaces nothing in the reference (a tuning knob, like craft_sim_tune). */
+/* Which kernel craft_step_teach launches: 0 (default) = the measured best (the step kernel
+ * with 2 teacher lanes per env for 3x3 windows, else the one-tile kernel with 4), 1 = the
+ * one-tile kernel, 2 = the two-tile kernel (3x3 windows and the default tile only), 3 = the
+ * step kernel (3x3 windows only); a choice a window does not support falls back to the
+ * one-tile kernel.  Results are identical for every setting.  Replaces nothing in the
+ * reference (a tuning knob, like craft_sim_tune). */
 int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel);
+
+/* Which kernel craft_step / craft_step_ex launch: 0 (default) = the step kernel
+ * (craft_step.h: every wave loads, steps, scatters and streams its own envs, no workgroup
+ * barrier), 1 = the tile kernel (craft_tile.h, round 1-2's tick kernel).  envs_per_wave: the
+ * step kernel's envs per tick wave (16, 32, 64; 0 = by batch size), per_cu: at most that many
+ * step workgroups per CU (pads the LDS request; 0 = no cap); both also apply to the step
+ * kernel of craft_step_teach.  Results are identical for every setting.  Replaces nothing in
+ * the reference (a tuning knob). */
+int craft_sim_tune_step(craft_sim_t* sim, int32_t kernel, int32_t envs_per_wave, int32_t per_cu);
+
+/* The kernel craft_step / craft_step_ex (teach == 0) or craft_step_teach (teach != 0) will
+ * launch, resolved from the knobs above: *kernel = CRAFT_KERNEL_STEP / _TILE / _TICK2, *envs =
+ * envs per tick wave (step kernel), per tile (tile kernel) or per workgroup (two-tile kernel),
+ * *lanes = teacher lanes per env (0 without a teacher).  Lets a caller (bench.py) name the
+ * kernel it times instead of mirroring the library's defaults. */
+#define CRAFT_KERNEL_STEP 0
+#define CRAFT_KERNEL_TILE 1
+#define CRAFT_KERNEL_TICK2 2
+int craft_sim_step_shape(const craft_sim_t* sim, int32_t teach, int32_t* kernel, int32_t* envs,
+                         int32_t* lanes);
 
 /* The launch shape the next craft_rollout will use, resolved from the knobs above:
  * envs per tile workgroup, threads per workgroup, and split = 1 for the

@@ -23,6 +23,8 @@ hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const Ti
                              hipStream_t st);
 hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
 size_t tick2_lds_bytes(int tl, int GS, int F);
+hipError_t launch_step(int win, int epw, size_t lds_min, const SimView& v, const TileArgs& a, hipStream_t st);
+hipError_t launch_step_teach(int epw, int nw, size_t lds_min, const SimView& v, const TileArgs& a, hipStream_t st);
 
 namespace {
 
@@ -152,7 +154,10 @@ struct craft_sim {
   bool sync_zeroed = false;         // d_sync zeroed once; then the counter only grows
   int rollout_obs_policy = 2;       // craft_rollout's observation stores until craft_sim_tune sets one:
                                     // write-through, 1.5 % faster than write-back (tools/ab_store.sh)
-  int teach_kernel = 0;             // craft_sim_tune_teach: 0 auto, 1 one-tile, 2 two-tile
+  int teach_kernel = 0;             // craft_sim_tune_teach: 0 auto, 1 one-tile, 2 two-tile, 3 step kernel
+  int step_kernel = 0;              // craft_sim_tune_step: 0 auto (the step kernel), 1 the tile kernel
+  int step_epw_knob = 0;            // craft_sim_tune_step: envs per tick wave (0 auto)
+  int step_per_cu = 0;              // craft_sim_tune_step: step workgroups per CU cap (0 none)
   uint64_t queue1_next = 0;         // queue[1] (the split kernel's per-unit path) at the next launch
   uint64_t queue_next = 0;          // the counter's value at the next launch (every launch adds
                                     // its units + its grid: one fetch past the end per workgroup)
@@ -255,15 +260,43 @@ void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
   *split = (t <= 32 && nt >= 320) ? 1 : 0;
 }
 
-// craft_step_teach runs the two-tile tick kernel (craft_tick2.h) for 3x3 windows at the default
-// tile shape from 32768 envs (tools/teacher_bench.py: 30.2 vs 38.1 us at 65536, level at 32768,
-// 19.4 vs 16.7 us at 4096, where its 128-env workgroups leave the chip a third full);
-// craft_sim_tune_teach forces either kernel.  The plain tick stays on the one-tile kernel: the
-// two-tile form measured 2-3 us slower without a teacher (tools/ab_tick2.sh).
-bool use_tick2(const craft_sim* s) {
-  if (s->cfg.window_width != 3 || s->tile != craft::kMaxTileEnvs || s->resident_cap != 0) return false;
-  if (s->teach_kernel) return s->teach_kernel == 2;
-  return s->n_envs >= 32768;
+// Envs per tick wave of the step kernel (craft_step.h): 64 once that still gives one 4-wave
+// workgroup per CU (256 workgroups at 65,536 envs), else 32, else 16 (4096 envs: 64 workgroups).
+int step_epw(const craft_sim* s) {
+  if (s->step_epw_knob) return s->step_epw_knob;
+  if (s->n_envs >= 65536) return 64;
+  if (s->n_envs >= 32768) return 32;
+  return 16;
+}
+
+// What craft_step / craft_step_ex (teach = false) or craft_step_teach (teach = true) launches:
+// CRAFT_KERNEL_STEP (craft_step.h), CRAFT_KERNEL_TILE (craft_tile.h) or CRAFT_KERNEL_TICK2
+// (craft_tick2.h), with its envs per tick wave / tile and teacher lanes per env.
+void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lanes) {
+  if (!teach) {
+    const bool step = s->step_kernel == 0;
+    *kernel = step ? 0 : 1;
+    *envs = step ? step_epw(s) : s->tile;
+    *lanes = 0;
+    return;
+  }
+  const bool w3 = s->cfg.window_width == 3;
+  int k = s->teach_kernel;
+  if (k == 0) k = w3 ? 3 : 1;
+  if ((k == 2 && !(w3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0)) || (k == 3 && !w3)) k = 1;
+  static const int tl2 = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 4) ? 4 : 2;
+  static const int tl1 = [] {
+    const char* e = getenv("CRAFT_TEACH_LANES");
+    const int x = e ? atoi(e) : 4;
+    return (x == 1 || x == 2) ? x : 4;
+  }();
+  if (k == 3) { *kernel = 0; *envs = step_epw(s); *lanes = 2; }
+  else if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
+  else { *kernel = 1; *envs = craft::kMaxTileEnvs; *lanes = tl1; }
+}
+
+size_t step_lds_min(const craft_sim* s) {
+  return s->step_per_cu > 0 ? (((size_t)163840 / s->step_per_cu) & ~size_t(15)) : 0;
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
@@ -420,9 +453,33 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
 
 int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel) {
   if (!s) return CRAFT_EINVAL;
-  if (kernel < 0 || kernel > 2)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile) or 2 (two-tile)");
+  if (kernel < 0 || kernel > 3)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile), 2 (two-tile) or 3 (step kernel)");
   s->teach_kernel = kernel;
+  return CRAFT_OK;
+}
+
+int craft_sim_tune_step(craft_sim_t* s, int32_t kernel, int32_t envs_per_wave, int32_t per_cu) {
+  if (!s) return CRAFT_EINVAL;
+  if (kernel < 0 || kernel > 1)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: kernel must be 0 (the step kernel) or 1 (the tile kernel)");
+  if (envs_per_wave != 0 && envs_per_wave != 16 && envs_per_wave != 32 && envs_per_wave != 64)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: envs_per_wave must be 0, 16, 32 or 64");
+  if (per_cu < 0 || per_cu > 16)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: per_cu must be 0..16");
+  s->step_kernel = kernel;
+  s->step_epw_knob = envs_per_wave;
+  s->step_per_cu = per_cu;
+  return CRAFT_OK;
+}
+
+int craft_sim_step_shape(const craft_sim_t* s, int32_t teach, int32_t* kernel, int32_t* envs, int32_t* lanes) {
+  if (!s) return CRAFT_EINVAL;
+  int k = 0, e = 0, l = 0;
+  step_shape(s, teach != 0, &k, &e, &l);
+  if (kernel) *kernel = k;
+  if (envs) *envs = e;
+  if (lanes) *lanes = l;
   return CRAFT_OK;
 }
 
@@ -656,26 +713,21 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   const int rc = step_args(s, x, a);
   if (rc != CRAFT_OK) return rc;
   a.label = label_out;
-  if (use_tick2(s)) {
-    // teacher lanes per env in the two-tile kernel: 2 (default) or 4 (CRAFT_TEACH_LANES=4, diagnostic)
-    static const int tl2 = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 4) ? 4 : 2;
-    hipError_t e = craft::launch_tick2(tl2, (s->view.C + 31) / 32, s->view, a,
-                                       craft::tick2_lds_bytes(tl2, s->view.GS, s->view.F),
-                                       reinterpret_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
-    return CRAFT_OK;
+  int kernel = 0, envs = 0, tl = 0;
+  step_shape(s, true, &kernel, &envs, &tl);
+  const int nw = (s->view.C + 31) / 32;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e;
+  if (kernel == 0) {
+    e = craft::launch_step_teach(envs, nw, step_lds_min(s), s->view, a, st);
+  } else if (kernel == 2) {
+    e = craft::launch_tick2(tl, nw, s->view, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
+  } else {
+    const int tile = craft::kMaxTileEnvs;
+    const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
+                       CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16;   // + task | frozen words, task_sub, D sync
+    e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, s->view, a, lds, st);
   }
-  // teacher lanes per env in the one-tile kernel: 4 (default), or 1 / 2 (CRAFT_TEACH_LANES, diagnostic)
-  static const int tl = [] {
-    const char* e = getenv("CRAFT_TEACH_LANES");
-    const int x = e ? atoi(e) : 4;
-    return (x == 1 || x == 2) ? x : 4;
-  }();
-  const int tile = craft::kMaxTileEnvs;
-  const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
-                     CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16;   // + task | frozen words, task_sub, D sync
-  hipError_t e = craft::launch_tick_teach(tl, (s->view.C + 31) / 32, s->cfg.window_width, s->view, a, lds,
-                                          reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
   return CRAFT_OK;
 }
@@ -685,6 +737,12 @@ int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
   TileArgs a;
   const int rc = step_args(s, x, a);
   if (rc != CRAFT_OK) return rc;
+  if (s->step_kernel == 0) {
+    hipError_t e = craft::launch_step(s->cfg.window_width, step_epw(s), step_lds_min(s), s->view, a,
+                                      reinterpret_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(s, e, "craft_step launch");
+    return CRAFT_OK;
+  }
   return launch(s, craft::MODE_TICK, a, stream, "craft_step launch");
 }
 

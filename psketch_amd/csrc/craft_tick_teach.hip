@@ -15,6 +15,12 @@ static hipError_t launch_tt(const SimView& v, const TileArgs& a, size_t lds, hip
   constexpr int TILE = kMaxTileEnvs;
   const int64_t tiles = (a.n + TILE - 1) / TILE;
   if (tiles == 0) return hipSuccess;
+  if (lds > 65536) {       // 5x5 / 7x7 windows: 64-env rows past 64 KiB (gfx950 allows 160 KiB)
+    if (lds > 163840) return hipErrorInvalidValue;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<WIN, MODE_TICK, TILE, TL, NW>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL((tile_kernel<WIN, MODE_TICK, TILE, TL, NW>), dim3((unsigned)tiles),
                      dim3(kThreads + TILE * TL), lds, st, v, a);
   return hipGetLastError();

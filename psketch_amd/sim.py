@@ -91,9 +91,26 @@ class CraftSim:
 
     def tune_teach(self, kernel=0):
         """Which kernel step(..., labels=) launches (craft_sim_tune_teach): 0 the
-        measured best, 1 the one-tile kernel, 2 the two-tile kernel (3x3 windows);
-        results are identical for every setting."""
+        measured best, 1 the one-tile kernel, 2 the two-tile kernel, 3 the step kernel
+        (3x3 windows); results are identical for every setting."""
         self._check(N.lib().craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
+
+    def tune_step(self, kernel=0, envs_per_wave=0, per_cu=0):
+        """Which kernel step() launches without labels (craft_sim_tune_step): 0 the step
+        kernel (default), 1 the tile kernel; the step kernel's envs per tick wave (0 = by
+        batch size) and workgroups-per-CU cap (0 = none); results are identical for every
+        setting."""
+        self._check(N.lib().craft_sim_tune_step(self._h, int(kernel), int(envs_per_wave), int(per_cu)),
+                    "craft_sim_tune_step")
+
+    def step_shape(self, teach=False):
+        """(kernel name, envs per wave / tile / workgroup, teacher lanes per env) that step()
+        launches, without (teach=False) or with labels= (craft_sim_step_shape)."""
+        k, e, l = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._check(N.lib().craft_sim_step_shape(self._h, int(bool(teach)), ctypes.byref(k),
+                                                 ctypes.byref(e), ctypes.byref(l)),
+                    "craft_sim_step_shape")
+        return N.KERNEL_NAMES[k.value], e.value, l.value
 
     def rollout_shape(self):
         """(tile_envs, threads, split) the next rollout() launches with, as the

@@ -1,0 +1,118 @@
+"""The one-launch-per-tick step kernel (csrc/craft_step.h), which craft_step / craft_step_ex /
+craft_step_teach launch by default: identical to the tile kernel (craft_tile.h) on every
+output of craft_step_ex across wave sizes, partial workgroups, windows and observation
+formats, and config 3's streamed tick (student actions, behaviour cloning, action record,
+any-live flag) at 65,536 envs against the CPU oracle (trainers/imitation.py:43-73 per env)."""
+import numpy as np
+import pytest
+import torch
+
+from psketch_amd import sample_scenarios, synthetic_specs
+from tests.helpers import make_tables
+from tests.test_gpu_parity import host, sim_with_pool
+
+pytestmark = pytest.mark.gpu
+
+
+def _outputs(sim, n, with_code=True):
+    dev = "cuda"
+    return {"obs": sim.empty_obs(), "reward": torch.empty(n, dtype=torch.float32, device=dev),
+            "done": torch.empty(n, dtype=torch.uint8, device=dev),
+            "success": torch.empty(n, dtype=torch.int8, device=dev),
+            "action_record": torch.empty(n, dtype=torch.int32, device=dev),
+            "any_live": torch.zeros(1, dtype=torch.int32, device=dev),
+            "transition_code": torch.empty(n, dtype=torch.int8, device=dev) if with_code else None}
+
+
+# n picks the envs per tick wave (64 from 65,536, 32 from 32,768, else 16) and leaves a partial
+# last workgroup (and wave); windows 5 and 7 use 8- and 4-env scatter sub-chunks
+@pytest.mark.parametrize("world,W,n,T,fmt,autoreset", [
+    ("craft_medium_12x12", 12, 70001, 12, "f32", True),
+    ("craft_medium_12x12", 12, 40000, 25, "f32", False),
+    ("craft_medium_12x12", 12, 5000, 25, "bf16", True),
+    ("craft_medium_12x12", 12, 1000, 25, "u8", False),
+    ("craft_medium_12x12_w5", 12, 3001, 25, "f32", True),
+    ("craft_medium_12x12_w5", 12, 33000, 10, "u8", True),
+    ("craft_16x16_w7", 16, 1000, 25, "f32", True),
+    ("craft_16x16_w7", 16, 999, 20, "bf16", False),
+    ("craft_medium", 8, 2000, 25, "f32", True)])
+def test_step_kernel_equals_tile_kernel(world, W, n, T, fmt, autoreset):
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 128)
+    specs = synthetic_specs(pool, W, W, n, 0, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    b.tune_step(1)
+    assert a.step_shape()[0] == "step_kernel" and b.step_shape()[0] == "tile_kernel"
+    assert a.step_shape()[1] == (64 if n >= 65536 else 32 if n >= 32768 else 16)
+    for s in (a, b):
+        s.set_obs_format(fmt)
+        s.reset(*specs)
+    oa, ob = _outputs(a, n), _outputs(b, n)
+    rng = np.random.RandomState(n)
+    for t in range(T):
+        acts = torch.as_tensor(rng.randint(0, 6, size=n).astype(np.int32), device="cuda")
+        ref = torch.as_tensor(rng.randint(0, 6, size=n).astype(np.int32), device="cuda")
+        bc = torch.as_tensor((rng.rand(n) < 0.3).astype(np.uint8), device="cuda")
+        hashed = t % 3 == 2                                       # the in-kernel draw on some ticks
+        for s, o in ((a, oa), (b, ob)):
+            o["any_live"].zero_()
+            s.step(None if hashed else acts, seed=7, tick=t, autoreset=autoreset,
+                   ref_actions=None if hashed else ref, behavior_clone=None if hashed else bc, **o)
+        for k in oa:
+            assert torch.equal(oa[k], ob[k]), f"{k} differs at tick {t}"
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
+    a.check()
+    b.check()
+
+
+def test_step_ex_streamed_tick_full_size_vs_oracle(oracle_mod):
+    """Config 3's tick as do_rollout issues it (trainers/imitation.py:43-73): 65,536 envs,
+    student actions, behaviour cloning from teacher-style labels, the action record and the
+    any-live flag, no auto-reset (done envs freeze), 40 ticks = one whole episode; every output
+    of 256 envs checked each tick against the oracle run on the same effective actions."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 1024)
+    n, T = 65536, 40
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=12, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    assert sim.step_shape() == ("step_kernel", 64, 0)
+    sim.reset(*specs)
+    out = _outputs(sim, n, with_code=False)
+    ids = np.sort(np.random.RandomState(5).choice(n, 256, replace=False))
+    o = oracle_mod.Oracle(cfg, pool)
+    envs = o.init_envs(*[x[ids] for x in specs])
+    rng = np.random.RandomState(6)
+    bc = (rng.rand(n) < 0.5).astype(np.uint8)               # config.random.binomial(1, mix, n)
+    bc_d = torch.as_tensor(bc, device="cuda")
+    frozen = np.zeros(n, dtype=bool)
+    for t in range(T):
+        student = rng.randint(0, 6, size=n).astype(np.int32)
+        ref = rng.randint(0, 6, size=n).astype(np.int32)
+        out["any_live"].zero_()
+        sim.step(torch.as_tensor(student, device="cuda"), tick=t, autoreset=False,
+                 ref_actions=torch.as_tensor(ref, device="cuda"), behavior_clone=bc_d, **out)
+        eff = np.where(bc == 1, ref, student)
+        pre_frozen = envs["frozen"].copy()
+        rc, oobs, orew, odone, osucc = o.batch_tick(envs, 0, eff[ids], 0, t, False)
+        assert rc == 0
+        np.testing.assert_array_equal(host(out["obs"])[ids], oobs, err_msg=f"obs t={t}")
+        np.testing.assert_array_equal(host(out["done"])[ids], odone, err_msg=f"done t={t}")
+        np.testing.assert_array_equal(host(out["success"])[ids], osucc, err_msg=f"success t={t}")
+        np.testing.assert_array_equal(host(out["reward"])[ids], orew, err_msg=f"reward t={t}")
+        rec = host(out["action_record"])
+        np.testing.assert_array_equal(rec[ids], np.where(pre_frozen != 0, -1, eff[ids]), err_msg=f"rec t={t}")
+        np.testing.assert_array_equal(rec, np.where(frozen, -1, eff), err_msg=f"rec (all) t={t}")
+        done = host(out["done"]).astype(bool)
+        frozen |= done
+        assert int(out["any_live"].item()) == int((~done).any()), t
+    assert frozen.all()                                     # timer 40: every episode has ended
+    st = {k: host(v) for k, v in sim.get_state(slots=torch.as_tensor(ids, dtype=torch.int32,
+                                                                         device="cuda")).items()}
+    np.testing.assert_array_equal(st["agent"], np.stack([envs["x"], envs["y"], envs["dir"], envs["timer"]], 1))
+    np.testing.assert_array_equal(st["inventory"], envs["inv"][:, :cfg.n_kinds])
+    np.testing.assert_array_equal(st["grid"], envs["grid"][:, :144])
+    sim.check()
