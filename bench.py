@@ -73,9 +73,12 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=1024)
     p.add_argument("--warmup", type=int, default=64)
-    p.add_argument("--workload", choices=("rollout", "teacher"), default="rollout",
+    p.add_argument("--workload", choices=("rollout", "teacher", "trainer"), default="rollout",
                    help="rollout: configs[2] (random rollout, full features); "
-                        "teacher: configs[4] (+ the BFS DemonstrationTeacher label every tick)")
+                        "teacher: configs[4] (+ the BFS DemonstrationTeacher label every tick); "
+                        "trainer: configs[2]/[4] closed loop, psketch_amd.rollout.do_rollout "
+                        "(train mode, fused teacher labels, a fixed on-device student); "
+                        "--steps counts rollouts")
     p.add_argument("--teacher-mode", choices=("fused", "separate"), default="fused",
                    help="teacher workload: one craft_step_teach launch per tick, or craft_teacher "
                         "then craft_step")
@@ -86,8 +89,8 @@ def parse(argv=None):
                    help="observation buffers cycled per tick (16 x 106 MB: 6.6x the Infinity Cache)")
     p.add_argument("--tile", type=int, default=0, help="envs per workgroup (0 = default)")
     p.add_argument("--obs-store", type=int, default=-1,
-                   help="0 write-back, 1 nontemporal, 2 sc1; -1: the measured best for the path "
-                        "(nontemporal for craft_step, write-through (sc1) for craft_rollout)")
+                   help="0 write-back, 1 nontemporal, 2 sc1; -1: the library default (write-through, "
+                        "sc1: the measured best for craft_rollout and for craft_step on a reused buffer)")
     p.add_argument("--ticks-per-launch", type=int, default=32,
                    help="K > 1: craft_rollout runs up to K ticks per launch (the same work per "
                         "tick); 1: one craft_step launch per tick")
@@ -244,7 +247,7 @@ def run(args):
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
-    obs_store = args.obs_store if args.obs_store >= 0 else (1 if K == 1 else 2)
+    obs_store = args.obs_store if args.obs_store >= 0 else 2
     sim.tune(args.tile, 0, obs_store)
     sim.set_obs_format(args.obs_format)
     sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
@@ -415,6 +418,188 @@ def run(args):
     D.shutdown()
 
 
+# ---- the closed-loop trainer workload (--workload trainer) ------------------------------------
+def trainer_policy(n_features, device, seed=7, L=4):
+    """A fixed student with tests/golden/imitation_rollout.npz's shape: scores = obs @ W[t % L] * 8
+    + bias, argmax over the 6 actions; small integer weights, so the fp32 GEMM is exact and the
+    policy has no side effects (do_rollout's lookahead may queue a tick ahead)."""
+    import torch
+    rng = np.random.RandomState(seed)
+    W = rng.randint(-3, 4, size=(L, n_features, 6))
+    bias = np.asarray([0, 1, 2, 3, 4, -8])
+    Wd = torch.as_tensor(W, dtype=torch.float32, device=device)
+    bd = torch.as_tensor(bias, dtype=torch.float32, device=device)
+
+    def act(obs, t):
+        return torch.addmm(bd, obs, Wd[t % L], alpha=8).argmax(dim=1).to(torch.int32)
+    return act, W, bias
+
+
+def cpu_baseline_trainer(cfg, grids, specs, W, bias, bc, seconds):
+    """oracle/rollout_oracle.py's do_rollout (trainers/imitation.py:18-101 one env at a time,
+    with the C oracle's step / features / DemonstrationTeacher) and the same fixed policy in
+    numpy, on rollouts of 256 envs of the same workload, one core."""
+    import oracle
+    from oracle import rollout_oracle
+    oracle.build()
+    o = oracle.Oracle(cfg, grids)
+    spec = np.stack(specs, axis=1)
+    pol = rollout_oracle.fake_policy(W, bias)
+    n, steps, rollouts = 256, 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and rollouts < 64:
+        lo = (rollouts * n) % len(spec)
+        sub = spec[lo:lo + n]
+        info = rollout_oracle.do_rollout(o, sub, pol, False, bc_mask=bc[lo:lo + n])
+        steps += n * max(len(r) for r in info["received"]) if info["received"] else 0
+        rollouts += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{rollouts} rollouts of {n} envs ({steps} env-ticks, {dt:.1f} s): "
+                      "oracle/rollout_oracle.py do_rollout (train mode, the C oracle's "
+                      "DemonstrationTeacher every live env every tick, behaviour cloning) with "
+                      "the same fixed policy in numpy, one core"}
+
+
+def run_trainer(args):
+    """configs[2]/[4] as a trainer runs them: psketch_amd.rollout.do_rollout (the whole
+    ImitationTrainer.do_rollout, trainers/imitation.py:18-101) per --steps rollout, train
+    mode: every tick the student's act() on the device observations, then one
+    craft_step_teach launch (behaviour cloning, the action record, the all(done) flag and the
+    DemonstrationTeacher's labels for the next tick), the flag read one tick behind
+    (lookahead).  Value = env slots x ticks / s over every rank."""
+    import torch
+    from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
+    from psketch_amd import distributed as D
+    from psketch_amd.rollout import do_rollout
+
+    rank, world_size, local_rank = D.world()
+    if args.one_device:
+        local_rank = 0
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    D.init(device=dev, backend=args.dist_backend)
+    env_base, n = D.env_shard(rank, args.envs)
+    sim = CraftSim(args.world, n_envs=n, device=local_rank, env_id_base=env_base,
+                   pool_capacity=args.pool)
+    grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
+    sim.load_pool(grids)
+    if args.obs_store >= 0:
+        sim.tune(args.tile, 0, args.obs_store)
+    tasks = [t.id for t in sim.task_manager.dataset_tasks()]
+    specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
+                            task_ids=tasks)
+    spec_d = [torch.as_tensor(a, device=dev) for a in specs]
+    act, W, bias = trainer_policy(sim.n_features, dev, seed=args.seed + 7)
+    bc = np.random.RandomState(args.seed + env_base).binomial(1, 0.5, size=n)
+    bc_d = torch.as_tensor(bc, device=dev)
+    received = []
+
+    def receive(r):                                  # student.receive keeps the labels
+        received.append(r)
+
+    def rollout():
+        received.clear()
+        return do_rollout(sim, spec_d, act, False, behavior_clone=bc_d, receive=receive,
+                          lookahead=True)
+
+    for _ in range(args.warmup):
+        rollout()
+    sim.check()
+    D.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ticks = live = 0
+    for _ in range(args.steps):
+        info = rollout()
+        ticks += info.ticks
+        live += info.num_interactions
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.barrier()
+    elapsed = D.max_over_ranks(t1 - t0, dev)
+    tot = D.reduce_episode_stats(torch.as_tensor([n * ticks, live, ticks], dtype=torch.int64,
+                                                 device=dev)).cpu().tolist()
+
+    # ---- per-tick split, outside the timed region: HIP events around the student's kernels
+    # and around each craft_step_teach launch of one more rollout ---------------------------
+    evs = {"policy": [], "env": []}
+    step0 = sim.step
+
+    def timed_act(obs, t):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = act(obs, t)
+        b.record()
+        evs["policy"].append((a, b))
+        return out
+
+    def timed_step(*a_, **k_):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = step0(*a_, **k_)
+        b.record()
+        evs["env"].append((a, b))
+        return out
+
+    sim.step = timed_step
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    info = do_rollout(sim, spec_d, timed_act, False, behavior_clone=bc_d, receive=receive,
+                      lookahead=True)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - w0) / max(1, len(evs["env"]))
+    sim.step = step0
+    pol_us = float(np.mean([a.elapsed_time(b) for a, b in evs["policy"]])) * 1e3
+    env_us = float(np.mean([a.elapsed_time(b) for a, b in evs["env"]])) * 1e3
+    sim.check()
+
+    if rank == 0:
+        win = sim.params["WINDOW_WIDTH"]
+        F = sim.n_features
+        kname, kenvs, lanes = sim.step_shape(teach=True)
+        bps = bytes_per_env_step(sim.width, sim.height, win, F, True, 4)
+        achieved = bps * n / (env_us * 1e-6) / 1e9
+        value = tot[0] / elapsed
+        line = {
+            "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: 1024 make_data.sample_scenario worlds (RandomState(123)), per-env "
+                    "init keyed by global id, a fixed integer-weight linear student, behaviour "
+                    "cloning mix 0.5",
+            "config": {"workload": f"{args.world}_w{win}_B{n}_trainer_closed_loop_train_fused_teacher",
+                       "world": args.world, "envs_per_gpu": n, "global_batch": n * world_size,
+                       "window": win, "n_features": F, "max_timesteps": sim.config.max_timesteps,
+                       "rollouts": args.steps, "ticks": tot[2], "step": "one do_rollout "
+                       "(ticks until every episode has ended, <= max_timesteps); value counts every "
+                       "env slot every tick", "lookahead": True,
+                       "parallelism": f"env-shard x{world_size}"},
+            "live_env_steps_per_s": tot[1] / elapsed,
+            "per_tick_us": {"wall": wall * 1e6, "policy": pol_us, "env_kernel": env_us,
+                            "host_gap": wall * 1e6 - pol_us - env_us},
+            "roofline": {"bound": "latency (tick prologue + BFS beside the observation stream)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": f"{kname} (craft_step_teach, {kenvs} envs, {lanes} teacher lanes)",
+                         "kernel_us": env_us, "bytes_per_env_step": bps,
+                         "bytes_per_launch": bps * n},
+        }
+        if world_size == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_trainer(sim.config, grids, specs, W, bias, bc,
+                                                        args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    D.shutdown()
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
@@ -424,7 +609,10 @@ def main(argv=None):
     if what != "run":
         print(f"bench.py: {what}", file=sys.stderr)
         return 2
-    run(args)
+    if args.workload == "trainer":
+        run_trainer(args)
+    else:
+        run(args)
     return 0
 
 

@@ -144,8 +144,8 @@ int craft_sim_info(const craft_sim_t* sim, int64_t* n_envs, int32_t* pool_capaci
  * window), the most tile workgroups that may share a CU (0 = no cap, else
  * 3..32), and the cache policy of the observation stores (0 write-back,
  * 1 nontemporal, 2 write-through) for every entry point.  Until it is called,
- * the tick kernels store nontemporal and craft_rollout write-through (each the
- * measured best).  Note: craft_sim_tune(.., 0, 0, 0) selects write-back. */
+ * every kernel stores write-through (sc1; the measured best for craft_rollout and for a
+ * tick that rewrites one buffer).  Note: craft_sim_tune(.., 0, 0, 0) selects write-back. */
 int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per_cu,
                    int32_t obs_store);
 
@@ -166,20 +166,19 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * for 3x3 windows, else the handle's tile with 256 threads (512 for 64-env tiles). */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
-/* Which kernel craft_step_teach launches: 0 (default) = the measured best (the step kernel
- * with 2 teacher lanes per env for 3x3 windows, else the one-tile kernel with 4), 1 = the
- * one-tile kernel, 2 = the two-tile kernel (3x3 windows and the default tile only), 3 = the
- * step kernel (3x3 windows only); a choice a window does not support falls back to the
- * one-tile kernel.  Results are identical for every setting.  Replaces nothing in the
+/* Which kernel craft_step_teach launches: 0 (default) = the measured best (the two-tile
+ * kernel with 2 teacher lanes per env for 3x3 windows at >= 32768 envs, else the one-tile
+ * kernel with 4), 1 = the one-tile kernel, 2 = the two-tile kernel (3x3 windows and the
+ * default tile only; otherwise the one-tile kernel).  Results are identical for every setting.  Replaces nothing in the
  * reference (a tuning knob, like craft_sim_tune). */
 int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel);
 
-/* Which kernel craft_step / craft_step_ex launch: 0 (default) = the step kernel
- * (craft_step.h: every wave loads, steps, scatters and streams its own envs, no workgroup
- * barrier), 1 = the tile kernel (craft_tile.h, round 1-2's tick kernel).  envs_per_wave: the
+/* Which kernel craft_step / craft_step_ex launch: 0 (default) = the measured best (the tile
+ * kernel), 1 = the tile kernel (craft_tile.h), 2 = the step kernel (craft_step.h: one
+ * workgroup per CU, tick waves that load, step and scatter beside stream waves that store).  envs_per_wave: the
  * step kernel's envs per tick wave (16, 32, 64; 0 = by batch size), per_cu: at most that many
- * step workgroups per CU (pads the LDS request; 0 = no cap); both also apply to the step
- * kernel of craft_step_teach.  Results are identical for every setting.  Replaces nothing in
+ * step workgroups per CU (pads the LDS request; 0 = no cap).  Results are identical for
+ * every setting.  Replaces nothing in
  * the reference (a tuning knob). */
 int craft_sim_tune_step(craft_sim_t* sim, int32_t kernel, int32_t envs_per_wave, int32_t per_cu);
 

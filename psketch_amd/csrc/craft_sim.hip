@@ -24,7 +24,6 @@ hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const Ti
 hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
 size_t tick2_lds_bytes(int tl, int GS, int F);
 hipError_t launch_step(int win, int epw, size_t lds_min, const SimView& v, const TileArgs& a, hipStream_t st);
-hipError_t launch_step_teach(int epw, int nw, size_t lds_min, const SimView& v, const TileArgs& a, hipStream_t st);
 
 namespace {
 
@@ -154,8 +153,8 @@ struct craft_sim {
   bool sync_zeroed = false;         // d_sync zeroed once; then the counter only grows
   int rollout_obs_policy = 2;       // craft_rollout's observation stores until craft_sim_tune sets one:
                                     // write-through, 1.5 % faster than write-back (tools/ab_store.sh)
-  int teach_kernel = 0;             // craft_sim_tune_teach: 0 auto, 1 one-tile, 2 two-tile, 3 step kernel
-  int step_kernel = 0;              // craft_sim_tune_step: 0 auto (the step kernel), 1 the tile kernel
+  int teach_kernel = 0;             // craft_sim_tune_teach: 0 auto, 1 one-tile, 2 two-tile
+  int step_kernel = 0;              // craft_sim_tune_step: 0 auto (the tile kernel), 1 tile, 2 step kernel
   int step_epw_knob = 0;            // craft_sim_tune_step: envs per tick wave (0 auto)
   int step_per_cu = 0;              // craft_sim_tune_step: step workgroups per CU cap (0 none)
   uint64_t queue1_next = 0;         // queue[1] (the split kernel's per-unit path) at the next launch
@@ -274,7 +273,9 @@ int step_epw(const craft_sim* s) {
 // (craft_tick2.h), with its envs per tick wave / tile and teacher lanes per env.
 void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lanes) {
   if (!teach) {
-    const bool step = s->step_kernel == 0;
+    // auto: the tile kernel (the step kernel measured 28.2-29.6 us against 26.1-26.5
+    // at 65,536 envs with a 16-slot ring, 23.3 against 20.3 with one reused buffer)
+    const bool step = s->step_kernel == 2;
     *kernel = step ? 0 : 1;
     *envs = step ? step_epw(s) : s->tile;
     *lanes = 0;
@@ -282,16 +283,17 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
   }
   const bool w3 = s->cfg.window_width == 3;
   int k = s->teach_kernel;
-  if (k == 0) k = w3 ? 3 : 1;
-  if ((k == 2 && !(w3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0)) || (k == 3 && !w3)) k = 1;
+  // auto: the two-tile kernel for 3x3 windows at the default tile from 32768 envs, where its
+  // 128-env workgroups fill the chip, else the one-tile kernel
+  if (k == 0) k = (w3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0 && s->n_envs >= 32768) ? 2 : 1;
+  if (k == 2 && !(w3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0)) k = 1;
   static const int tl2 = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 4) ? 4 : 2;
   static const int tl1 = [] {
     const char* e = getenv("CRAFT_TEACH_LANES");
     const int x = e ? atoi(e) : 4;
     return (x == 1 || x == 2) ? x : 4;
   }();
-  if (k == 3) { *kernel = 0; *envs = step_epw(s); *lanes = 2; }
-  else if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
+  if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
   else { *kernel = 1; *envs = craft::kMaxTileEnvs; *lanes = tl1; }
 }
 
@@ -341,7 +343,9 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   s->n_envs = n_envs;
   s->env_base = env_id_base;
   s->pool_capacity = pool_capacity;
-  s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs;   // stats rows
+  // stats rows: one per 16-env tile, plus the step kernel's last workgroup's tick waves (its
+  // wave count is rounded up to the workgroup's 4)
+  s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs + 4;
   // default tile: the observation rows staged in LDS stay near 40 KB per workgroup
   s->tile = cfg->window_width == 3 ? 64 : (cfg->window_width == 5 ? 32 : 16);
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
@@ -421,7 +425,10 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.W = W; v.H = H; v.K = K; v.F = F; v.C = C; v.CS = CS; v.GS = GS;
   v.maxT = cfg->max_timesteps;
   v.bridge = cfg->bridge_kind;
-  v.obs_policy = 1;   // nontemporal observation stores (fastest in tools/sweep_tiles.py)
+  // write-through (sc1) observation stores: with one observation buffer rewritten every tick (a
+  // trainer's, do_rollout's) the tick kernel takes 20.3 us against 26.4 with nontemporal stores,
+  // and 27.0 against 26.5 when every tick writes a fresh slot of a 1.7 GB ring (tools/step_probe.py)
+  v.obs_policy = 2;
   v.obs_fmt = CRAFT_OBS_F32;
   v.axe = cfg->axe_kind;
   v.kc_lo = v.kc_hi = 0;
@@ -453,16 +460,16 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
 
 int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel) {
   if (!s) return CRAFT_EINVAL;
-  if (kernel < 0 || kernel > 3)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile), 2 (two-tile) or 3 (step kernel)");
+  if (kernel < 0 || kernel > 2)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile) or 2 (two-tile)");
   s->teach_kernel = kernel;
   return CRAFT_OK;
 }
 
 int craft_sim_tune_step(craft_sim_t* s, int32_t kernel, int32_t envs_per_wave, int32_t per_cu) {
   if (!s) return CRAFT_EINVAL;
-  if (kernel < 0 || kernel > 1)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: kernel must be 0 (the step kernel) or 1 (the tile kernel)");
+  if (kernel < 0 || kernel > 2)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: kernel must be 0 (auto), 1 (the tile kernel) or 2 (the step kernel)");
   if (envs_per_wave != 0 && envs_per_wave != 16 && envs_per_wave != 32 && envs_per_wave != 64)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: envs_per_wave must be 0, 16, 32 or 64");
   if (per_cu < 0 || per_cu > 16)
@@ -718,9 +725,7 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   const int nw = (s->view.C + 31) / 32;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
-  if (kernel == 0) {
-    e = craft::launch_step_teach(envs, nw, step_lds_min(s), s->view, a, st);
-  } else if (kernel == 2) {
+  if (kernel == 2) {
     e = craft::launch_tick2(tl, nw, s->view, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
   } else {
     const int tile = craft::kMaxTileEnvs;
@@ -737,7 +742,7 @@ int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
   TileArgs a;
   const int rc = step_args(s, x, a);
   if (rc != CRAFT_OK) return rc;
-  if (s->step_kernel == 0) {
+  if (s->step_kernel == 2) {
     hipError_t e = craft::launch_step(s->cfg.window_width, step_epw(s), step_lds_min(s), s->view, a,
                                       reinterpret_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(s, e, "craft_step launch");

@@ -83,34 +83,52 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   if (wave < J) {
     // ---- A + C: wave j, one lane per env of tile j (as tile_kernel<MODE_TICK>) -------------------
     const int j = wave;
-    // each of these waves copies the tables it reads (identical values)
-    for (int t = lane; t < v.n_tasks; t += 64) s_task[t] = v.task_tab[t];
-    if (TL > 0)
-      for (int t = lane; t < v.n_tasks * CRAFT_MAX_SUBTASKS; t += 64) s_tsub[t] = v.task_sub[t];
-    for (int t = lane; t < CRAFT_MAX_RECIPES * 3; t += 64) s_rc[t] = v.rcw[t];
-
     const int nE = tile_envs(j);
     const int le = j * kTick2Tile + lane;                                // env index in the workgroup
     const int64_t slot = envw + le;
     bool live = lane < nE;
     uint32_t init_word = 0;
-    int act = 0;
+    int act = 0, ref = 0;
+    uint32_t bc = 0;
+    uint64_t st = 0;
     uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0, m0 = i0, m1 = i0;
     Agent s{};
+    // every independent load first, no result used before the last is issued (a wave waits for
+    // its loads in issue order): one round trip, then the scenario row
     if (live) {
-      const uint64_t st = v.state[slot];
-      init_word = v.init[slot];
-      if (a.actions) {
-        act = a.actions[slot];
-      } else {
-        const uint64_t gid = (uint64_t)(v.env_base + slot);
-        act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)a.tick) >> 32) % 6u);
-      }
-      if (a.bc && a.bc[slot]) act = a.ref[slot];                        // behaviour cloning, imitation.py:56-57
+      st = v.state[slot];
       i0 = v.inv[2 * slot];
       i1 = v.inv[2 * slot + 1];
       m0 = v.mask[2 * slot];
       m1 = v.mask[2 * slot + 1];
+      init_word = v.init[slot];
+      if (a.actions) act = a.actions[slot];
+      if (a.bc) {
+        bc = a.bc[slot];
+        ref = a.ref[slot];
+      }
+    }
+    // each of these waves copies the tables it reads (identical values); unconditional loads
+    // within the tables' allocations, in the same round trip
+    const uint32_t tw = v.task_tab[lane];
+    const uint32_t rw = v.rcw[min(lane, CRAFT_MAX_RECIPES * 3 - 1)];
+    int32_t sw[CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64];
+#pragma unroll
+    for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q) sw[q] = TL > 0 ? v.task_sub[lane + 64 * q] : 0;
+    if (lane < v.n_tasks) s_task[lane] = (uint16_t)tw;
+    if (lane < CRAFT_MAX_RECIPES * 3) s_rc[lane] = rw;
+    if (TL > 0) {
+#pragma unroll
+      for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q)
+        if (lane + 64 * q < v.n_tasks * CRAFT_MAX_SUBTASKS) s_tsub[lane + 64 * q] = sw[q];
+    }
+    if (live) {
+      if (!a.actions) {
+        const uint64_t gid = (uint64_t)(v.env_base + slot);
+        act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)a.tick) >> 32) % 6u);
+      }
+      asm volatile("" : "+v"(bc), "+v"(ref));                          // (no early wait on the flag)
+      if (a.bc && (bc & 0xffu)) act = ref;                             // behaviour cloning, imitation.py:56-57
       s = unpack_state(st);
       if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
         latch_error(v.err, CRAFT_EINVAL, slot);                          // never initialised

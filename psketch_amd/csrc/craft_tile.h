@@ -52,17 +52,12 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
   STAMP(0);
   // ---- A + C: wave 0, one lane per env ------------------------------------------------------
   if (tid < TILE) {
-    for (int t = tid; t < v.n_tasks; t += TILE) s_task[t] = v.task_tab[t];
-    if (TL > 0) {
-      for (int t = tid; t < v.n_tasks * CRAFT_MAX_SUBTASKS; t += TILE) s_tsub[t] = v.task_sub[t];
-      if (tid == 0) *s_dsync = 0u;
-    }
-    for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += TILE) s_rc[t] = v.rcw[t];
-
     int64_t slot = 0, dslot = 0;
     bool live = tid < nE;
     uint32_t init_word = 0;
-    int act = 0;
+    int act = 0, ref = 0;
+    uint32_t bc = 0;
+    uint64_t st = 0;
     uint4 i0 = make_uint4(0, 0, 0, 0), i1 = i0, m0 = i0, m1 = i0;
     Agent s{};
     if (live) {
@@ -73,6 +68,51 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
         latch_error(v.err, CRAFT_ERANGE, i);
         live = false;
       }
+    }
+    // Every independent load of the env first, no result used before the last is issued (a
+    // wave waits for its loads in issue order): state, inventory, mask, restart spec, action and
+    // clone flag + label, then the static tables into registers; one round trip, then the row.
+    if (live && MODE != MODE_RESET) {
+      st = v.state[slot];
+      i0 = v.inv[2 * slot];
+      i1 = v.inv[2 * slot + 1];
+      m0 = v.mask[2 * slot];
+      m1 = v.mask[2 * slot + 1];
+      if (MODE == MODE_TICK || MODE == MODE_TRANSITION) init_word = v.init[slot];
+      if (MODE == MODE_TICK) {
+        if (a.actions) act = a.actions[slot];
+        if (a.bc) {
+          bc = a.bc[slot];
+          ref = a.ref[slot];
+        }
+      } else if (MODE == MODE_TRANSITION) {
+        act = a.actions[env0 + tid];
+      }
+    }
+    constexpr int QT = (CRAFT_MAX_TASKS + TILE - 1) / TILE;
+    constexpr int QR = (CRAFT_MAX_RECIPES * 3 + TILE - 1) / TILE;
+    constexpr int QS = TL > 0 ? (CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS + TILE - 1) / TILE : 1;
+    uint32_t tw[QT], rw[QR];
+    int32_t sw[QS];
+    // (unconditional loads within the tables' allocations: straight-line code, no wait between)
+#pragma unroll
+    for (int q = 0; q < QT; ++q) tw[q] = v.task_tab[min(tid + q * TILE, CRAFT_MAX_TASKS - 1)];
+#pragma unroll
+    for (int q = 0; q < QR; ++q) rw[q] = v.rcw[min(tid + q * TILE, CRAFT_MAX_RECIPES * 3 - 1)];
+#pragma unroll
+    for (int q = 0; q < QS; ++q)
+      sw[q] = TL > 0 ? v.task_sub[min(tid + q * TILE, CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS - 1)] : 0;
+#pragma unroll
+    for (int q = 0; q < QT; ++q)
+      if (tid + q * TILE < v.n_tasks) s_task[tid + q * TILE] = (uint16_t)tw[q];
+#pragma unroll
+    for (int q = 0; q < QR; ++q)
+      if (tid + q * TILE < CRAFT_MAX_RECIPES * 3) s_rc[tid + q * TILE] = rw[q];
+    if (TL > 0) {
+#pragma unroll
+      for (int q = 0; q < QS; ++q)
+        if (tid + q * TILE < v.n_tasks * CRAFT_MAX_SUBTASKS) s_tsub[tid + q * TILE] = sw[q];
+      if (tid == 0) *s_dsync = 0u;
     }
     if (live) {
       if (MODE == MODE_RESET) {
@@ -86,23 +126,14 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
           s.x = x0; s.y = y0; s.dir = d0; s.frozen = 0; s.timer = v.maxT; s.scen = sc; s.task = tk;
         }
       } else {
-        const uint64_t st = v.state[slot];
-        if (MODE == MODE_TICK || MODE == MODE_TRANSITION) init_word = v.init[slot];
         if (MODE == MODE_TICK) {
-          if (a.actions) {
-            act = a.actions[slot];
-          } else {
+          if (!a.actions) {
             const uint64_t gid = (uint64_t)(v.env_base + slot);
             act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)a.tick) >> 32) % 6u);
           }
-          if (a.bc && a.bc[slot]) act = a.ref[slot];    // behaviour cloning, imitation.py:56-57
-        } else if (MODE == MODE_TRANSITION) {
-          act = a.actions[env0 + tid];
+          asm volatile("" : "+v"(bc), "+v"(ref));                      // (no early wait on the flag)
+          if (a.bc && (bc & 0xffu)) act = ref;                         // behaviour cloning, imitation.py:56-57
         }
-        i0 = v.inv[2 * slot];
-        i1 = v.inv[2 * slot + 1];
-        m0 = v.mask[2 * slot];
-        m1 = v.mask[2 * slot + 1];
         s = unpack_state(st);
         if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
           latch_error(v.err, CRAFT_EINVAL, slot);   // never initialised by reset / set_state

@@ -17,6 +17,8 @@ tick, imitation.py:42).  After the loop, `distances` (imitation.py:79-91) come
 from the same teacher kernel: failed get-tasks are reset to their initial grid
 at their final position and find_closest_resources' length is read back.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -57,7 +59,7 @@ class RolloutInfo:
 
 
 def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_obs=False,
-               timing=None, fused_teacher=True):
+               timing=None, fused_teacher=True, lookahead=False):
     """One rollout of sim.n_envs episodes.
 
     spec: (scenario, x, y, dir, task), each n_envs ints (device or host).
@@ -73,8 +75,16 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     fused_teacher: when not is_eval, each tick's step also labels the new states
       (craft_step_teach: the next tick's ref_actions, in the same launch);
       False runs craft_teacher on a side stream, overlapping the student.
+    lookahead: the all(done) test of tick t (imitation.py:42) no longer blocks the
+      host before tick t + 1 is queued: the any-live flag is copied to pinned host
+      memory behind an event, tick t + 1 (act and step) is queued, and only then is the
+      flag read.  When tick t ended every episode the queued tick is discarded: its step
+      is a no-op on frozen envs (no state, counter, success or action-record change that
+      the result keeps), but act was called once more than the reference calls it, so
+      lookahead is for side-effect-free students (a fixed or deterministic policy);
+      receive() is still called exactly once per real tick.  Needs is_eval or the fused
+      teacher.
     """
-    import time
     t_start = time.perf_counter()
     n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
     if T <= 0:
@@ -124,6 +134,25 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
         else:
             launch_teacher()
     t_loop = time.perf_counter()
+    if lookahead:
+        if not is_eval and not fused_teacher:
+            raise ValueError("lookahead needs is_eval or fused_teacher")
+        t = _lookahead_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs,
+                            live, ref, ref_next, bc, T, n, dev)
+    else:
+        t = _sync_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs, live,
+                       ref, ref_next, bc, T, n, dev, fused_teacher, side, main, labels_ready,
+                       launch_teacher)
+    if side is not None:
+        main.wait_stream(side)
+    t_end_loop = time.perf_counter()
+    return _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot_ids,
+                   timing, t_start, t_loop, t_end_loop, dev)
+
+
+def _sync_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs, live, ref,
+               ref_next, bc, T, n, dev, fused_teacher, side, main, labels_ready, launch_teacher):
+    """The reference's loop order: every tick's all(done) is read back before the next act."""
     t = 0
     while True:
         actions = act(obs, t)
@@ -149,9 +178,59 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
         # every env is done once its timer reaches 0 (imitation.py:42, 62-63)
         if t >= T or int(live[t - 1]) == 0:
             break
-    if side is not None:
-        main.wait_stream(side)
-    t_end_loop = time.perf_counter()
+    return t
+
+
+def _lookahead_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs, live,
+                    ref, ref_next, bc, T, n, dev):
+    """do_rollout's loop with tick t + 1 queued before tick t's all(done) flag is read
+    (see do_rollout's lookahead).  Returns the number of real ticks."""
+    flags = getattr(sim, "_live_host", None)
+    if flags is None or flags.numel() < T:                 # pinned, reused across rollouts
+        flags = sim._live_host = torch.zeros(max(T, 64), dtype=torch.int32, pin_memory=True)
+        sim._live_events = [torch.cuda.Event() for _ in range(flags.numel())]
+    events = sim._live_events
+    fused = not is_eval
+    cur = {"obs": obs, "ref": ref, "ref_next": ref_next}
+
+    def issue(t):
+        """act + step of tick t on the stream, then the flag copy behind an event; returns the
+        clone of the tick's ref_actions for receive() (taken before a later tick overwrites them)."""
+        o = cur["obs"]
+        actions = act(o, t)
+        if not torch.is_tensor(actions):
+            actions = torch.as_tensor(np.asarray(actions), device=dev)
+        actions = actions.to(device=dev, dtype=torch.int32).reshape(n)
+        if keep_obs:
+            cur["obs"] = obs_hist[t + 1]
+        sim.step(actions, tick=t, autoreset=False, obs=cur["obs"], success=success,
+                 ref_actions=None if is_eval else cur["ref"], behavior_clone=bc,
+                 action_record=seqs[t], any_live=live[t:t + 1],
+                 labels=cur["ref_next"] if fused else None)
+        got = cur["ref"].clone() if (fused and receive is not None) else None
+        flags[t:t + 1].copy_(live[t:t + 1], non_blocking=True)
+        events[t].record()
+        if fused:
+            cur["ref"], cur["ref_next"] = cur["ref_next"], cur["ref"]
+        return got
+
+    pending = issue(0)
+    t = 0
+    while True:
+        nxt = issue(t + 1) if t + 1 < T else None           # queued before the flag is read
+        events[t].synchronize()
+        if fused and receive is not None:
+            receive(pending)                                 # tick t is real
+        t += 1
+        if t >= T or int(flags[t - 1]) == 0:
+            break                                            # a queued tick t is discarded
+        pending = nxt
+    return t
+
+
+def _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot_ids, timing,
+            t_start, t_loop, t_end_loop, dev):
+    n = sim.n_envs
     # distances (imitation.py:79-91): failed get tasks, initial grid at the final pose
     get_ids = getattr(sim, "_get_task_ids", None)
     if get_ids is None:

@@ -91,15 +91,15 @@ class CraftSim:
 
     def tune_teach(self, kernel=0):
         """Which kernel step(..., labels=) launches (craft_sim_tune_teach): 0 the
-        measured best, 1 the one-tile kernel, 2 the two-tile kernel, 3 the step kernel
-        (3x3 windows); results are identical for every setting."""
+        measured best, 1 the one-tile kernel, 2 the two-tile kernel (3x3 windows); results
+        are identical for every setting."""
         self._check(N.lib().craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
 
     def tune_step(self, kernel=0, envs_per_wave=0, per_cu=0):
-        """Which kernel step() launches without labels (craft_sim_tune_step): 0 the step
-        kernel (default), 1 the tile kernel; the step kernel's envs per tick wave (0 = by
-        batch size) and workgroups-per-CU cap (0 = none); results are identical for every
-        setting."""
+        """Which kernel step() launches without labels (craft_sim_tune_step): 0 the measured
+        best (the tile kernel), 1 the tile kernel, 2 the step kernel; the step kernel's envs
+        per tick wave (0 = by batch size) and workgroups-per-CU cap (0 = none); results are
+        identical for every setting."""
         self._check(N.lib().craft_sim_tune_step(self._h, int(kernel), int(envs_per_wave), int(per_cu)),
                     "craft_sim_tune_step")
 

@@ -21,10 +21,13 @@ def torch_policy(W, bias, device):
 
 
 @pytest.mark.parametrize("case", ["dev8", "w12"])
-@pytest.mark.parametrize("mode,fused", [("train", True), ("train", False), ("eval", True)])
-def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode, fused):
+@pytest.mark.parametrize("mode,fused,lookahead", [("train", True, False), ("train", False, False),
+                                                  ("eval", True, False), ("train", True, True),
+                                                  ("eval", True, True)])
+def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode, fused, lookahead):
     """fused: the teacher labels come from each step's launch (craft_step_teach); else from
-    craft_teacher on a side stream."""
+    craft_teacher on a side stream.  lookahead: tick t + 1 is queued before tick t's all(done)
+    flag is read; the result, every receive() call included, must not change."""
     from psketch_amd import CraftSim
     from psketch_amd.rollout import do_rollout
     fx = golden("imitation_rollout.npz")
@@ -36,7 +39,8 @@ def test_do_rollout_matches_reference_fixture(golden, gpu, case, mode, fused):
     received = []
     info = do_rollout(sim, tuple(spec.T), torch_policy(fx[f"{case}_W"], fx[f"{case}_bias"], gpu),
                       mode == "eval", behavior_clone=fx[key + "_bc"],
-                      receive=lambda r: received.append(r.cpu().numpy()), fused_teacher=fused)
+                      receive=lambda r: received.append(r.cpu().numpy()), fused_teacher=fused,
+                      lookahead=lookahead)
     ref = info.to_reference()
     A = fx[key + "_action_seqs"]
     assert ref["action_seqs"] == [[int(a) for a in row if a >= 0] for row in A]
@@ -115,3 +119,42 @@ def test_imitation_rollout_replays_dataset(golden, gpu):
     assert total == len(ds)
     # last batch has a different size: a second simulator was created for it
     assert len(runner._sims) == 2
+
+
+@pytest.mark.parametrize("is_eval,keep_obs", [(False, False), (True, True)])
+def test_lookahead_equals_sync_loop_full_size(gpu, is_eval, keep_obs):
+    """Config 3/5 size (65,536 envs): the lookahead loop gives the synchronous loop's result
+    bit for bit: action_seqs, success, distances, counters, every receive() call, ticks and
+    (keep_obs) every observation; a policy that stops most episodes early makes the loop end
+    before the timer, so the discarded speculative tick is exercised."""
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import do_rollout
+    from psketch_amd.sim import sample_scenarios, synthetic_specs
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 256)
+    n = 65536
+    spec = synthetic_specs(pool, 12, 12, n, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
+    rng = np.random.RandomState(4)
+    W = rng.randint(-3, 4, size=(4, cfg.n_features, 6))
+    bias = np.asarray([0, 1, 2, 3, 4, 6])                 # STOP is favoured: early all-done
+    bc = rng.binomial(1, 0.5, size=n)
+    outs = []
+    for lookahead in (False, True):
+        sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+        sim.load_pool(pool)
+        received = []
+        info = do_rollout(sim, spec, torch_policy(W, bias, gpu), is_eval, behavior_clone=bc,
+                          receive=lambda r: received.append(r.cpu().numpy()), keep_obs=keep_obs,
+                          lookahead=lookahead)
+        outs.append((info, received))
+    (a, ra), (b, rb) = outs
+    assert a.ticks == b.ticks and a.ticks < cfg.max_timesteps
+    for k in ("action_seqs", "n_actions", "success", "distances"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    assert (a.num_interactions, a.num_steps) == (b.num_interactions, b.num_steps)
+    assert len(ra) == len(rb) == (0 if is_eval else a.ticks)
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x, y)
+    if keep_obs:
+        assert torch.equal(a.obs, b.obs)

@@ -1,8 +1,8 @@
-"""The one-launch-per-tick step kernel (csrc/craft_step.h), which craft_step / craft_step_ex /
-craft_step_teach launch by default: identical to the tile kernel (craft_tile.h) on every
-output of craft_step_ex across wave sizes, partial workgroups, windows and observation
-formats, and config 3's streamed tick (student actions, behaviour cloning, action record,
-any-live flag) at 65,536 envs against the CPU oracle (trainers/imitation.py:43-73 per env)."""
+"""The one-launch-per-tick kernels: the step kernel (csrc/craft_step.h, craft_sim_tune_step 2)
+identical to the tile kernel (craft_tile.h, the default) on every output of craft_step_ex
+across wave sizes, partial workgroups, windows and observation formats; and config 3's
+streamed tick (student actions, behaviour cloning, action record, any-live flag) at 65,536
+envs on the default kernel against the CPU oracle (trainers/imitation.py:43-73 per env)."""
 import numpy as np
 import pytest
 import torch
@@ -41,6 +41,7 @@ def test_step_kernel_equals_tile_kernel(world, W, n, T, fmt, autoreset):
     pool, _, _ = sample_scenarios(params, cb, 123, 128)
     specs = synthetic_specs(pool, W, W, n, 0, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
     a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.tune_step(2)
     b.tune_step(1)
     assert a.step_shape()[0] == "step_kernel" and b.step_shape()[0] == "tile_kernel"
     assert a.step_shape()[1] == (64 if n >= 65536 else 32 if n >= 32768 else 16)
@@ -79,7 +80,7 @@ def test_step_ex_streamed_tick_full_size_vs_oracle(oracle_mod):
     n, T = 65536, 40
     specs = synthetic_specs(pool, 12, 12, n, 0, seed=12, task_ids=[t.id for t in tm.dataset_tasks()])
     sim = sim_with_pool(world, n, pool)
-    assert sim.step_shape() == ("step_kernel", 64, 0)
+    assert sim.step_shape() == ("tile_kernel", 64, 0)                 # the default
     sim.reset(*specs)
     out = _outputs(sim, n, with_code=False)
     ids = np.sort(np.random.RandomState(5).choice(n, 256, replace=False))

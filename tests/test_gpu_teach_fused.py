@@ -14,23 +14,21 @@ from tests.test_gpu_parity import host, sim_with_pool
 pytestmark = pytest.mark.gpu
 
 
-# kernel: 0 the library's choice (the step kernel, craft_step.h, for 3x3 windows), 1 the one-tile
-# kernel (craft_tile.h), 2 the two-tile kernel (craft_tick2.h), 3 the step kernel (3x3 windows
-# only; 2 and 3 fall back to the one-tile kernel elsewhere)
+# kernel: 0 the library's choice (the two-tile kernel for 3x3 windows from 32768 envs), 1 the
+# one-tile kernel (craft_tile.h), 2 the two-tile kernel (craft_tick2.h; the one-tile kernel for
+# other windows)
 @pytest.mark.parametrize("world,W,n,T,autoreset,given,kernel", [
     ("craft_medium_12x12", 12, 65536, 45, True, False, 0),  # config 5's size, across episode ends
     ("craft_medium_12x12", 12, 5000, 45, False, True, 2),   # frozen envs (label -1), a partial tile
     ("craft_medium_12x12", 12, 5000, 45, False, True, 1),
-    ("craft_medium_12x12", 12, 40000, 45, False, True, 3),  # 32 envs per tick wave, partial workgroup
-    ("craft_medium_12x12", 12, 70001, 12, True, True, 3),   # 64 envs per tick wave, partial wave
-    ("craft_medium", 8, 3000, 30, True, True, 3),
+    ("craft_medium_12x12", 12, 40000, 45, False, True, 2),  # partial last workgroup
+    ("craft_medium_12x12", 12, 70001, 12, True, True, 0),
     ("craft_medium_12x12", 12, 4000, 30, True, True, 0),
     ("craft_medium", 8, 3000, 30, True, True, 2),           # 8x8: two words per cell set
     ("craft_medium", 8, 3000, 30, True, True, 1),
     ("craft_medium_12x12_w5", 12, 2048, 20, True, False, 2),  # w = 5: always the one-tile kernel
     ("craft_large", 10, 1024, 20, True, False, 2),          # 10x10: four words per cell set
-    ("craft_large", 10, 1024, 20, True, False, 1),
-    ("craft_large", 10, 1000, 20, True, False, 3)])
+    ("craft_large", 10, 1024, 20, True, False, 1)])
 def test_step_teach_equals_step_then_teacher(world, W, n, T, autoreset, given, kernel):
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 256)

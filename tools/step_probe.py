@@ -24,6 +24,8 @@ def main():
     p.add_argument("--ring", type=int, nargs="+", default=[16, 1])
     p.add_argument("--iters", type=int, default=200)
     p.add_argument("--teacher", action="store_true")
+    p.add_argument("--obs-store", type=int, nargs="+", default=[1],
+                   help="observation store policies to time (craft_sim_tune: 0 wb, 1 nt, 2 sc1)")
     p.add_argument("--cfg", nargs="+", default=["0:0"],
                    help="step kernel knobs EPW:PER_CU (craft_sim_tune_step; 0 = auto / no cap)")
     args = p.parse_args()
@@ -70,23 +72,30 @@ def main():
                      labels=lab[r])
             st["t"] += 1
 
-        res = {"world": args.world, "envs": n, "ring": R, "fill_us": round(timeit(fill, args.iters), 2)}
-        sim.tune_step(1)
-        res["tile_us"] = round(timeit(step, args.iters), 2)
-        for cfg in args.cfg:
-            epw, per_cu = (int(x) for x in cfg.split(":"))
-            sim.tune_step(0, epw, per_cu)
-            res[f"step_{cfg}_us"] = round(timeit(step, args.iters), 2)
-        sim.tune_step(0)
-        if args.teacher:
-            for k, name in ((2, "teach_tick2"), (1, "teach_tile")):
-                sim.tune_teach(k)
-                res[f"{name}_us"] = round(timeit(teach, args.iters), 2)
-            sim.tune_teach(3)
+        res = {"world": args.world, "envs": n, "ring": R, "fill_us": round(timeit(fill, args.iters), 2),
+               "stream_env": os.environ.get("CRAFT_STEP_STREAM", "")}
+        for pol in args.obs_store:
+            sim.tune(0, 0, pol)
+            sim.tune_step(1)
+            res[f"tile_p{pol}_us"] = round(timeit(step, args.iters), 2)
             for cfg in args.cfg:
                 epw, per_cu = (int(x) for x in cfg.split(":"))
-                sim.tune_step(0, epw, per_cu)
-                res[f"teach_step_{cfg}_us"] = round(timeit(teach, args.iters), 2)
+                sim.tune_step(2, epw, per_cu)
+                res[f"step_{cfg}_p{pol}_us"] = round(timeit(step, args.iters), 2)
+        sim.tune(0, 0, 2)
+        sim.tune_step(0)
+        if args.teacher:
+            for pol in args.obs_store:
+                sim.tune(0, 0, pol)
+                for k, name in ((2, "teach_tick2"), (1, "teach_tile")):
+                    sim.tune_teach(k)
+                    res[f"{name}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
+                sim.tune_teach(3)
+                for cfg in args.cfg:
+                    epw, per_cu = (int(x) for x in cfg.split(":"))
+                    sim.tune_step(2, epw, per_cu)
+                    res[f"teach_step_{cfg}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
+            sim.tune(0, 0, 2)
             sim.tune_step(0)
             sim.tune_teach(0)
         print(json.dumps(res), flush=True)

@@ -5,8 +5,8 @@ Links psketch_amd/lib/libpsketch_craft_diag.so from the product objects except c
 craft_step, which are compiled again with -DCRAFT_STAMPS (never the product library), then
 runs 20 craft_step ticks at 65,536 envs (ring of 16 observation slots) per knob setting and
 reports, in µs from the launch's first stamp (percentiles over tick waves): tick wave start,
-A (loads landed), C, the workgroup barrier, the first and last scatter published, the stream
-wave's stores drained, and the number of tick waves per CU.
+A (loads landed), C, the first and last scatter published, the stream wave's first sub-chunk
+issued and its stores drained, and the number of tick waves per CU.
 
     python tools/step_stamps.py [--build] [--cfg EPW:PER_CU ...]"""
 import argparse
@@ -69,12 +69,12 @@ def main():
                                [t.id for t in sim.task_manager.dataset_tasks()]))
     R = 16
     ring = torch.empty((R, n, sim.n_features), dtype=torch.float32, device="cuda")
-    rows = (n + 15) // 16
+    rows = 2 * ((n + 15) // 16)                            # + the extra stamps (STEP_STAMP2)
     st = torch.zeros((rows, 8), dtype=torch.int64, device="cuda")
     tick = 0
     for cfg in args.cfg:
         epw, per_cu = (int(x) for x in cfg.split(":"))
-        sim.tune_step(0, epw, per_cu)
+        sim.tune_step(2, epw, per_cu)
         res = []
         for t in range(20):
             lib.craft_debug_set_stamps(sim._h, ctypes.c_void_p(st.data_ptr() if t >= 5 else 0))
@@ -85,16 +85,20 @@ def main():
             if t < 5:
                 continue
             w = (n + epw - 1) // epw
+            nw = ((n + 4 * epw - 1) // (4 * epw)) * 4           # tick waves of the launch
             s = st[:w].cpu().numpy()
-            res.append(s)
+            s2 = st[nw:nw + w].cpu().numpy()
+            res.append(np.concatenate([s, s2[:, :5]], axis=1))
         lib.craft_debug_set_stamps(sim._h, ctypes.c_void_p(0))
         r = np.stack(res)                                   # [ticks, waves, 8]
-        tm = r[:, :, :7].astype(np.float64) / 100.0         # 100 MHz -> µs
+        tm = np.concatenate([r[:, :, :7], r[:, :, 8:13]], axis=2).astype(np.float64) / 100.0   # µs
         t0 = tm[:, :, 0].min(axis=1, keepdims=True)
         rel = tm - t0[:, :, None]
         out = {"epw": epw, "per_cu": per_cu, "kernel_span_med": round(float(np.median(rel[:, :, 6].max(1))), 2)}
-        names = [("start", 0), ("A_done", 1), ("C_done", 2), ("barrier", 3), ("D0_published", 4),
-                 ("D_all_published", 5), ("stream_drained", 6)]
+        names = [("start", 0), ("A1_landed", 7), ("pool_issued", 11), ("pool_landed", 8), ("A_done", 1),
+                 ("C_done", 2), ("D0_first", 9),
+                 ("D0_repeat", 10), ("D0_published", 3), ("D_all_published", 4), ("E0_issued", 5),
+                 ("stream_drained", 6)]
         for nm, k in names:
             out[nm] = [round(float(np.percentile(rel[:, :, k], q)), 2) for q in (10, 50, 90, 100)]
         hw = r[0, :, 7]
