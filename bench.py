@@ -170,11 +170,14 @@ def _cores():
     return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n))))
 
 
-def cpu_baseline_c(cfg, grids, specs, env_id_base, seed, seconds):
-    """The C restatement (oracle/craft_oracle.c oracle_bench) on a bounded sample
-    of the same workload, one thread per host core given to this job, each on
-    its own contiguous slice of global env ids, every env writing its own
-    observation row; env-steps/s.  ctypes releases the GIL around each call."""
+def cpu_baseline_c(cfg, grids, specs, env_id_base, seed, seconds, teacher=False, ring=16):
+    """The C restatement (oracle/craft_oracle.c oracle_bench) on a bounded sample of the same
+    workload, one thread per host core given to this job, each on its own contiguous slice of
+    global env ids, every env writing its own observation row into ring slot tick % ring of a
+    per-thread ring (16 slots x 256 envs x 1616 B = 6.6 MB per thread, 106 MB over 16 threads:
+    past the threads' cache share, so the stores reach DRAM as the GPU's do); with `teacher`
+    (configs[4]) the DemonstrationTeacher labels every env's new state every tick, as
+    craft_step_teach does.  env-steps/s.  ctypes releases the GIL around each call."""
     import threading
     import oracle
     oracle.build()
@@ -184,7 +187,7 @@ def cpu_baseline_c(cfg, grids, specs, env_id_base, seed, seconds):
     envs = o.init_envs(*[a[:n] for a in specs])
     bounds = np.linspace(0, n, cores + 1).astype(int)
     parts = [(envs[bounds[i]:bounds[i + 1]].copy(), env_id_base + int(bounds[i])) for i in range(cores)]
-    bufs = [o.bench_buffers(len(p[0])) for p in parts]
+    bufs = [o.bench_buffers(len(p[0]), ring, teacher) for p in parts]
     steps = [0] * cores
     ticks = [0] * cores
     t0 = time.perf_counter()
@@ -203,11 +206,15 @@ def cpu_baseline_c(cfg, grids, specs, env_id_base, seed, seconds):
         t.join()
     dt = time.perf_counter() - t0
     total = sum(steps)
+    what = ("step + satisfies + full features() + the DemonstrationTeacher's BFS label of every "
+            "env's new state" if teacher else "step + satisfies + full features()")
     return {"value": total / dt, "unit": "env-steps/s", "cores": cores, "kind": "port",
             "sample": f"{n} envs x {total // n} ticks ({dt:.1f} s) of the same workload (12x12 "
-                      "craft_medium, global-id hashed actions, auto-reset): step + satisfies + full "
-                      "features() with obs/reward/done/success written to each env's own row; "
-                      f"oracle/craft_oracle.c (gcc -O3), {cores} threads on contiguous env slices"}
+                      f"craft_medium, global-id hashed actions, auto-reset): {what}, obs/reward/"
+                      f"done/success written to each env's own row, observations cycled through a "
+                      f"{ring}-slot ring per thread ({ring * 256 * 1616 // 2**20} MB per thread of "
+                      f"256 envs: stores reach DRAM); oracle/craft_oracle.c (gcc -O3), {cores} "
+                      "threads on contiguous env slices"}
 
 
 def cpu_baseline_numpy(cfg, grids, specs, env_id_base, seed, seconds):
@@ -224,6 +231,50 @@ def cpu_baseline_numpy(cfg, grids, specs, env_id_base, seed, seconds):
 
 
 # ---- the GPU run -----------------------------------------------------------------------------
+def fill_ceiling(bufs, reps=8):
+    """In-situ write ceiling: GB/s of torch's zero_ fill over the same buffers the
+    timed kernels write, one fill launch per buffer, cycled like the kernels cycle them, timed
+    with HIP events after one warm pass.  Returns (GB/s, µs per buffer)."""
+    import torch
+    for b in bufs:
+        b.zero_()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        for b in bufs:
+            b.zero_()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    nbytes = sum(b.numel() * b.element_size() for b in bufs) * reps
+    return nbytes / (ms * 1e-3) / 1e9, ms * 1e3 / (reps * len(bufs))
+
+
+
+def profiled_kernel_us(fn, m, name):
+    """Mean device duration (µs) of the kernels whose name contains `name` over m calls of fn(),
+    from the torch profiler's device activity (roctracer on ROCm: the same launch records as
+    rocprofv3 --kernel-trace), or None when the profiler yields no such kernel.  Unlike a pair of
+    HIP events around back-to-back launches it excludes the dispatch gaps between launches."""
+    import torch
+    from torch.profiler import ProfilerActivity, profile
+    try:
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            for _ in range(m):
+                fn()
+            torch.cuda.synchronize()
+        durs = [e.device_time if hasattr(e, "device_time") else e.cuda_time
+                for e in prof.events() if name in e.name and getattr(e, "device_type", None) is not None
+                and str(e.device_type).endswith("CUDA")]
+        durs = [d for d in durs if d and d > 0]
+        return float(np.mean(durs)) if durs else None
+    except Exception:                               # no device tracer on this build
+        return None
+
+
+
 def run(args):
     import torch
     from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
@@ -289,6 +340,9 @@ def run(args):
                             success=success)
             tick += k
 
+    # the in-situ write ceiling of the same ring, slot by slot (before the warmup, so that the
+    # timed region follows the kernel's own warm launches)
+    ceiling_gbs, ceiling_slot_us = fill_ceiling([ring[r] for r in range(R)], reps=4)
     for k in warm_plan:
         launch(k)
     sim.check()
@@ -322,6 +376,16 @@ def run(args):
     ev1.record(kstream)
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / m                                # per launch (k_eff ticks)
+    # one launch per tick (craft_step / craft_step_teach): price the kernel's own duration (the
+    # profiler's device records, as rocprof reports them), not launches plus dispatch gaps
+    prof_us = None
+    if K == 1:
+        if teacher and args.teacher_mode == "fused":
+            pname = {"tile_kernel": "tile_kernel", "tick2_kernel": "tick2_kernel",
+                     "step_kernel": "step_kernel"}[sim.step_shape(teach=True)[0]]
+        else:
+            pname = sim.step_shape()[0]
+        prof_us = profiled_kernel_us(lambda: launch(1), min(m, 64), pname)
 
     # ---- scalar episode summary: one RCCL all-reduce of int64[3] ----------------------------
     stats = D.reduce_episode_stats(sim.stats()).cpu().tolist()
@@ -343,19 +407,15 @@ def run(args):
                      "rollout_unit_ticks": (k_eff if args.rollout_chunk <= 0 else args.rollout_chunk),
                      "rollout_pipeline": "continuous" if args.rollout_chunk == -1 else "per unit"}
         else:
-            tile, _ = sim.tile_shape()
-            kname = f"tile_kernel<{win}, MODE_TICK, {tile}>"
-            if teacher and args.teacher_mode == "fused":
-                nw = (sim.width * sim.height + 31) // 32
-                # craft_sim.hip use_tick2: the two-tile kernel for 3x3 windows at the default
-                # tile from 32768 envs
-                kname = (f"tick2_kernel<3, 2, 4, 2, {nw}> (craft_step_teach)"
-                         if win == 3 and tile == 64 and n >= 32768
-                         else f"tile_kernel<{win}, MODE_TICK, 64, 4, {nw}> (craft_step_teach)")
-            elif teacher:
+            # what the library launches (craft_sim_step_shape), not a mirror of its defaults
+            kn, kenvs, lanes = sim.step_shape(teach=teacher and args.teacher_mode == "fused")
+            kname = f"{kn}<{win}> ({kenvs} envs per {'wave' if kn == 'step_kernel' else 'workgroup'}"
+            kname += f", {lanes} teacher lanes per env) (craft_step_teach)" if lanes else ") (craft_step)"
+            if teacher and args.teacher_mode != "fused":
                 kname += " + teacher_kernel"
-            shape = {"tile": tile}
-        achieved = bps * n * k_eff / (kernel_ms * 1e-3) / 1e9
+            shape = {"tile": kenvs, "kernel": kn, "teacher_lanes": lanes}
+        kernel_us_priced = prof_us if prof_us is not None else kernel_ms * 1e3
+        achieved = bps * n * k_eff / (kernel_us_priced * 1e-6) / 1e9
         workload = f"{args.world}_w{win}_B{n}_" + (
             "teacher_labels_full_features" if teacher else "random_rollout_full_features")
         if K > 1:
@@ -376,6 +436,13 @@ def run(args):
                         traffic = e.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
+        if teacher:
+            bound = ("latency: the tick's prologue plus the BFS beside the observation stream "
+                     "(store floor of the tick's bytes at the in-situ ceiling below)")
+        elif K == 1:
+            bound = "hbm (one launch per tick: plus the tick's latency-bound prologue)"
+        else:
+            bound = "hbm"
         line = {
             "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
             "value": value,
@@ -400,14 +467,22 @@ def run(args):
                             "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
                             "launches": len(timed_plan),
                             "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]}, **shape),
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-                         "kernel_us": kernel_ms * 1e3, "ticks_per_launch": k_eff,
-                         "bytes_per_launch": bps * n * k_eff, "bytes_per_env_step": bps},
+                         "kernel_us": kernel_us_priced,
+                         "kernel_us_source": "torch profiler device records (as rocprof)" if prof_us
+                         is not None else "HIP events over back-to-back launches",
+                         "kernel_us_events": kernel_ms * 1e3, "ticks_per_launch": k_eff,
+                         "bytes_per_launch": bps * n * k_eff, "bytes_per_env_step": bps,
+                         "ceiling_gbs": ceiling_gbs, "frac_of_ceiling": achieved / ceiling_gbs,
+                         "ceiling": f"torch zero_ of each {R}-slot ring buffer in turn "
+                                    f"({ceiling_slot_us:.1f} us per {ring[0].numel() * ring.element_size() / 1e6:.0f} MB "
+                                    "slot), measured in this run before the timed region"},
             "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},
         }
         if world_size == 1 and not args.no_cpu_baseline:
-            c_leg = cpu_baseline_c(sim.config, grids, specs, env_base, args.seed, args.cpu_seconds)
+            c_leg = cpu_baseline_c(sim.config, grids, specs, env_base, args.seed, args.cpu_seconds,
+                                   teacher=teacher)
             try:
                 np_leg = cpu_baseline_numpy(sim.config, grids, specs, env_base, args.seed,
                                             args.cpu_seconds)
@@ -506,6 +581,9 @@ def run_trainer(args):
     for _ in range(args.warmup):
         rollout()
     sim.check()
+    ceil_buf = sim.empty_obs()          # do_rollout rewrites one observation buffer every tick
+    ceiling_gbs, ceiling_us = fill_ceiling([ceil_buf], reps=16)
+    del ceil_buf
     D.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -521,37 +599,28 @@ def run_trainer(args):
     tot = D.reduce_episode_stats(torch.as_tensor([n * ticks, live, ticks], dtype=torch.int64,
                                                  device=dev)).cpu().tolist()
 
-    # ---- per-tick split, outside the timed region: HIP events around the student's kernels
-    # and around each craft_step_teach launch of one more rollout ---------------------------
-    evs = {"policy": [], "env": []}
-    step0 = sim.step
+    # ---- per-tick split, outside the timed region: HIP events at the start and the end of the
+    # student's kernels of every tick of one more rollout; the env launch (craft_step_teach,
+    # and the flag's 4-byte copy) runs between one tick's policy end and the next one's start ----
+    marks = []
 
     def timed_act(obs, t):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         out = act(obs, t)
         b.record()
-        evs["policy"].append((a, b))
+        marks.append((a, b))
         return out
 
-    def timed_step(*a_, **k_):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        out = step0(*a_, **k_)
-        b.record()
-        evs["env"].append((a, b))
-        return out
-
-    sim.step = timed_step
     torch.cuda.synchronize()
     w0 = time.perf_counter()
     info = do_rollout(sim, spec_d, timed_act, False, behavior_clone=bc_d, receive=receive,
                       lookahead=True)
     torch.cuda.synchronize()
-    wall = (time.perf_counter() - w0) / max(1, len(evs["env"]))
-    sim.step = step0
-    pol_us = float(np.mean([a.elapsed_time(b) for a, b in evs["policy"]])) * 1e3
-    env_us = float(np.mean([a.elapsed_time(b) for a, b in evs["env"]])) * 1e3
+    wall = (time.perf_counter() - w0) / max(1, info.ticks)
+    pol_us = float(np.mean([a.elapsed_time(b) for a, b in marks[:info.ticks]])) * 1e3
+    env_us = float(np.mean([marks[k][1].elapsed_time(marks[k + 1][0])
+                            for k in range(min(info.ticks, len(marks) - 1))])) * 1e3
     sim.check()
 
     if rank == 0:
@@ -585,13 +654,20 @@ def run_trainer(args):
                        "parallelism": f"env-shard x{world_size}"},
             "live_env_steps_per_s": tot[1] / elapsed,
             "per_tick_us": {"wall": wall * 1e6, "policy": pol_us, "env_kernel": env_us,
-                            "host_gap": wall * 1e6 - pol_us - env_us},
+                            "host_gap": wall * 1e6 - pol_us - env_us,
+                            "note": "one instrumented rollout after the timed region: HIP events "
+                                    "at the start and end of the student's kernels; env_kernel = "
+                                    "policy end to the next tick's policy start (the "
+                                    "craft_step_teach launch and the any-live flag copy)"},
             "roofline": {"bound": "latency (tick prologue + BFS beside the observation stream)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": f"{kname} (craft_step_teach, {kenvs} envs, {lanes} teacher lanes)",
                          "kernel_us": env_us, "bytes_per_env_step": bps,
-                         "bytes_per_launch": bps * n},
+                         "bytes_per_launch": bps * n, "ceiling_gbs": ceiling_gbs,
+                         "frac_of_ceiling": achieved / ceiling_gbs,
+                         "ceiling": f"torch zero_ of one [n, F] fp32 buffer rewritten in place, as "
+                                    f"do_rollout's observation buffer is ({ceiling_us:.1f} us per fill)"},
         }
         if world_size == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_trainer(sim.config, grids, specs, W, bias, bc,

@@ -309,7 +309,12 @@ int craft_step_teach(craft_sim_t* sim, const craft_step_args_t* args, int32_t* l
  * observations: `actions` is device int32[n_ticks][n_envs] or NULL for the
  * hashed draw.  Tick t writes ring slot t % ring of each output: obs
  * [ring][n_envs][n_features] (obs format; each slot 16-byte aligned), reward /
- * done / success [ring][n_envs]; each may be NULL. */
+ * done / success [ring][n_envs]; each may be NULL.
+ * Ordering: one handle's craft_rollout launches must run in issue order, i.e. on one stream (or
+ * streams the caller orders): the work-unit counter they share is advanced by each launch, not
+ * re-zeroed.  A launch captured into a HIP graph (hipStreamIsCapturing) uses a separate counter
+ * that a memset captured with it zeroes, so a graph may be replayed any number of times, in
+ * order with each other and with eager launches. */
 int craft_rollout(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed, int64_t tick0,
                   int32_t n_ticks, uint32_t flags, void* obs, int32_t ring, float* reward,
                   uint8_t* done, int8_t* success, void* stream);

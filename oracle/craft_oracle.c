@@ -284,15 +284,27 @@ int oracle_batch_tick(const craft_config_t* cfg, const uint8_t* pool, oracle_env
 
 int64_t oracle_bench(const craft_config_t* cfg, const uint8_t* pool, oracle_env_t* envs,
                      int64_t n, int64_t env_id_base, int64_t tick0, int64_t ticks, uint64_t seed,
-                     float* obs, float* reward, uint8_t* done, int8_t* success, int64_t* stats) {
+                     float* obs, int32_t ring, float* reward, uint8_t* done, int8_t* success,
+                     int32_t* labels, int64_t* stats) {
   /* The GPU bench's work, tick for tick: the do_rollout protocol with hashed
    * actions keyed by global id, auto-reset, and every output written to its own
-   * row (obs [n][F], reward/done/success [n]) — the same stores the GPU is
-   * charged for. */
-  for (int64_t t = 0; t < ticks; ++t)
+   * row (obs [n][F] in ring slot tick % ring, reward/done/success [n]) — the same
+   * stores the GPU is charged for; with `labels`, the DemonstrationTeacher
+   * (teachers/demonstration.py:9-30) of every env's new state too (config 5:
+   * craft_step_teach), -1 for a frozen env, -2 where the reference raises. */
+  const int64_t slot = n * (int64_t)cfg->n_features;
+  for (int64_t t = 0; t < ticks; ++t) {
+    float* o = obs ? obs + ((tick0 + t) % (ring > 0 ? ring : 1)) * slot : NULL;
     if (oracle_batch_tick(cfg, pool, envs, n, env_id_base, NULL, seed, tick0 + t,
-                          CRAFT_STEP_AUTORESET, obs, reward, done, success, stats))
+                          CRAFT_STEP_AUTORESET, o, reward, done, success, stats))
       return -1;
+    if (labels)
+      for (int64_t e = 0; e < n; ++e) {
+        int32_t a = -1;
+        if (!envs[e].frozen && oracle_teacher(cfg, &envs[e], envs[e].task, &a)) a = -2;
+        labels[e] = a;
+      }
+  }
   return n * ticks;
 }
 

@@ -78,7 +78,8 @@ int oracle_batch_tick(const craft_config_t* cfg, const uint8_t* pool, oracle_env
  * (own row per env, as the GPU does).  Returns env-steps run, -1 on error. */
 int64_t oracle_bench(const craft_config_t* cfg, const uint8_t* pool, oracle_env_t* envs,
                      int64_t n, int64_t env_id_base, int64_t tick0, int64_t ticks, uint64_t seed,
-                     float* obs, float* reward, uint8_t* done, int8_t* success, int64_t* stats);
+                     float* obs, int32_t ring, float* reward, uint8_t* done, int8_t* success,
+                     int32_t* labels, int64_t* stats);
 
 /* make_data.sample_scenario (make_data.py:105-144) with random_free
  * (make_data.py:74-103) and all_free_cells_reachable (make_data.py:27-72),

@@ -149,6 +149,7 @@ struct craft_sim {
   int rollout_chunk = 0;            // craft_rollout ticks per work unit (0: the whole launch)
   int rollout_threads = 0;          // craft_rollout threads per tile workgroup (0: 8 per env)
   uint8_t* d_sync = nullptr;        // craft_rollout: work-unit counter + per-tile chunk flags
+  uint8_t* d_sync_graph = nullptr;  // the same for launches captured into a HIP graph
   size_t sync_bytes = 0;
   bool sync_zeroed = false;         // d_sync zeroed once; then the counter only grows
   int rollout_obs_policy = 2;       // craft_rollout's observation stores until craft_sim_tune sets one:
@@ -398,6 +399,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_err, 4 * sizeof(int32_t));
   s->sync_bytes = (16 + 4 * (size_t)((n_envs + 15) / 16) + 15) & ~size_t(15);   // queue + tile_done
   ALLOC(s->d_sync, s->sync_bytes);
+  ALLOC(s->d_sync_graph, s->sync_bytes);      // craft_rollout launches captured into a graph
 #undef ALLOC
   if ((e = hipMemcpy(s->d_task, task_tab.data(), sizeof(uint16_t) * task_tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "task table");
@@ -524,6 +526,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_stats);
   (void)hipFree(s->d_err);
   (void)hipFree(s->d_sync);
+  (void)hipFree(s->d_sync_graph);
   delete s;
   return CRAFT_OK;
 }
@@ -772,8 +775,16 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   a.done = done;
   a.sat = success;
   a.chunk = s->rollout_chunk > 0 ? s->rollout_chunk : (n_ticks > 0 ? n_ticks : 1);
-  a.queue = reinterpret_cast<unsigned long long*>(s->d_sync);
-  a.tile_done = reinterpret_cast<uint32_t*>(s->d_sync + 16);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // A launch captured into a HIP graph (torch.cuda.graph) is replayed without this host code, so
+  // it cannot use the eager launches' running counter: it gets its own sync area, zeroed by a
+  // memset captured with it, so every replay starts from zero and never touches the eager one.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(s, hipStreamIsCapturing(st, &cap));
+  const bool captured = cap != hipStreamCaptureStatusNone;
+  uint8_t* sync = captured ? s->d_sync_graph : s->d_sync;
+  a.queue = reinterpret_cast<unsigned long long*>(sync);
+  a.tile_done = reinterpret_cast<uint32_t*>(sync + 16);
   int tile = 0, threads = 0, split = 0;
   rollout_shape(s, &tile, &threads, &split);
   // chunk_ticks -1: the split kernel's continuous pipeline (its 3x3 default shape, observations
@@ -786,23 +797,29 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   // handed between workgroups) also need zeroed per-tile flags: those zero the whole area.
   const int64_t n_chunks = n_ticks > 0 ? (n_ticks + a.chunk - 1) / a.chunk : 0;
   const int64_t units = ((s->n_envs + tile - 1) / tile) * n_chunks;
-  if (n_ticks > 0 && (n_chunks > 1 || !s->sync_zeroed)) {
-    HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, reinterpret_cast<hipStream_t>(stream)));
-    s->sync_zeroed = true;
-    s->queue_next = 0;
-    s->queue1_next = 0;
+  if (captured) {
+    if (n_ticks > 0) HIP_TRY(s, hipMemsetAsync(sync, 0, s->sync_bytes, st));
+    a.qbase = 0;
+    a.qbase1 = 0;
+  } else {
+    if (n_ticks > 0 && (n_chunks > 1 || !s->sync_zeroed)) {
+      HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, st));
+      s->sync_zeroed = true;
+      s->queue_next = 0;
+      s->queue1_next = 0;
+    }
+    a.qbase = s->queue_next;
+    a.qbase1 = s->queue1_next;
   }
-  a.qbase = s->queue_next;
-  a.qbase1 = s->queue1_next;
   int64_t grid = 0;
   a.grid_out = &grid;
   SimView view = s->view;
   view.obs_policy = s->rollout_obs_policy;
-  hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, view, a, lds_bytes(s, tile, 2, true),
-                                       reinterpret_cast<hipStream_t>(stream));
+  hipError_t e = craft::launch_rollout(s->cfg.window_width, tile, threads, view, a, lds_bytes(s, tile, 2, true), st);
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout launch");
   // the split kernel's per-unit path counts on queue[1] (craft_rollout_split.h), the others on
   // queue[0]
+  if (captured) return CRAFT_OK;
   if (grid > 0 && split && !flat) s->queue1_next += (uint64_t)std::max<int64_t>(units, grid);
   else if (grid > 0) s->queue_next += (uint64_t)(units + grid);
   return CRAFT_OK;

@@ -17,11 +17,13 @@ tick, imitation.py:42).  After the loop, `distances` (imitation.py:79-91) come
 from the same teacher kernel: failed get-tasks are reset to their initial grid
 at their final position and find_closest_resources' length is read back.
 """
+import ctypes
 import time
 
 import numpy as np
 import torch
 
+from . import _native as N
 from .sim import CraftSim
 
 GOAL_GET = "get"
@@ -98,9 +100,10 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     sim.reset(*spec, obs=obs)
     success = torch.zeros(n, dtype=torch.int8, device=dev)
     seqs = torch.full((T, n), -1, dtype=torch.int32, device=dev)
-    live = torch.zeros(T, dtype=torch.int32, device=dev)     # 1: some env still running after tick t
-    ref = torch.empty(n, dtype=torch.int32, device=dev)
-    ref_next = torch.empty(n, dtype=torch.int32, device=dev) if fused_teacher else None
+    live = torch.zeros(T + 1, dtype=torch.int32, device=dev)  # 1: some env still running after tick t
+    # ref_actions of every tick: tick t reads refs[t] and (fused) labels refs[t + 1]; receive()
+    # gets the row itself (no copy), which no later tick or rollout overwrites
+    refs = None if is_eval else torch.empty((T + 1, n), dtype=torch.int32, device=dev)
     bc = None
     if not is_eval:
         if behavior_clone is None:
@@ -109,9 +112,12 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
                              else behavior_clone, device=dev)
         if bc.numel() != n:
             raise ValueError(f"behavior_clone has {bc.numel()} entries, expected {n}")
-        bc = (bc.reshape(n) != 0).to(torch.uint8)
-    # The teacher reads only the env states, so tick t's labels are computed on a
-    # side stream while the student's act(t) runs on the main stream.
+        bc = (bc.reshape(n) != 0).to(torch.uint8).contiguous()
+    fused = not is_eval and fused_teacher
+    if lookahead and not is_eval and not fused_teacher:
+        raise ValueError("lookahead needs is_eval or fused_teacher")
+    # The teacher reads only the env states, so without the fused teacher tick t's labels are
+    # computed on a side stream while the student's act(t) runs on the main stream.
     main = torch.cuda.current_stream(dev)
     side = None
     if not is_eval and not fused_teacher:
@@ -122,27 +128,49 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     if labels_ready is None:
         labels_ready = sim._teacher_event = torch.cuda.Event()
 
-    def launch_teacher():
-        side.wait_stream(main)                   # after the previous step (and receive's copy)
+    def launch_teacher(t):
+        side.wait_stream(main)                   # after the previous step
         with torch.cuda.stream(side):
-            sim.teacher(action_out=ref)          # done (frozen) envs get -1
+            sim.teacher(action_out=refs[t])      # done (frozen) envs get -1
         labels_ready.record(side)
+
+    step = _stepper(sim, fused, bc, success)
+    cur = {"obs": obs}
+
+    def issue(t):
+        """Tick t on the stream: the student's act, then one step launch (behaviour cloning, the
+        action record, the any-live flag and, fused, the next tick's labels)."""
+        actions = act(cur["obs"], t)
+        if not torch.is_tensor(actions):
+            actions = torch.as_tensor(np.asarray(actions), device=dev)
+        actions = actions.to(device=dev, dtype=torch.int32).reshape(n).contiguous()
+        if side is not None:
+            main.wait_event(labels_ready)
+        if keep_obs:
+            cur["obs"] = obs_hist[t + 1]
+        step(t, actions, cur["obs"], None if is_eval else refs[t], seqs[t], live[t:t + 1],
+             refs[t + 1] if fused else None)
+        if side is not None and t + 1 < T:
+            launch_teacher(t + 1)                # speculative: all -1 if every env is done
 
     if not is_eval:
         if fused_teacher:
-            sim.teacher(action_out=ref)          # the initial states' labels; then every step's
+            sim.teacher(action_out=refs[0])      # the initial states' labels; then every step's
         else:
-            launch_teacher()
+            launch_teacher(0)
     t_loop = time.perf_counter()
     if lookahead:
-        if not is_eval and not fused_teacher:
-            raise ValueError("lookahead needs is_eval or fused_teacher")
-        t = _lookahead_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs,
-                            live, ref, ref_next, bc, T, n, dev)
+        t = _lookahead_loop(sim, issue, receive, is_eval, refs, live, T)
     else:
-        t = _sync_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs, live,
-                       ref, ref_next, bc, T, n, dev, fused_teacher, side, main, labels_ready,
-                       launch_teacher)
+        t = 0
+        while True:
+            issue(t)
+            if not is_eval and receive is not None:
+                receive(refs[t])
+            t += 1
+            # every env is done once its timer reaches 0 (imitation.py:42, 62-63)
+            if t >= T or int(live[t - 1]) == 0:
+                break
     if side is not None:
         main.wait_stream(side)
     t_end_loop = time.perf_counter()
@@ -150,81 +178,58 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
                    timing, t_start, t_loop, t_end_loop, dev)
 
 
-def _sync_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs, live, ref,
-               ref_next, bc, T, n, dev, fused_teacher, side, main, labels_ready, launch_teacher):
-    """The reference's loop order: every tick's all(done) is read back before the next act."""
-    t = 0
-    while True:
-        actions = act(obs, t)
-        if not torch.is_tensor(actions):
-            actions = torch.as_tensor(np.asarray(actions), device=dev)
-        actions = actions.to(device=dev, dtype=torch.int32).reshape(n)
-        if not is_eval and not fused_teacher:
-            main.wait_event(labels_ready)
-        if keep_obs:
-            obs = obs_hist[t + 1]
-        fused = not is_eval and fused_teacher
-        sim.step(actions, tick=t, autoreset=False, obs=obs, success=success,
-                 ref_actions=None if is_eval else ref, behavior_clone=bc,
-                 action_record=seqs[t], any_live=live[t:t + 1],
-                 labels=ref_next if fused else None)
-        if not is_eval and receive is not None:
-            receive(ref.clone())
-        t += 1
-        if fused:
-            ref, ref_next = ref_next, ref        # this step's labels are the next tick's ref_actions
-        elif not is_eval and t < T:
-            launch_teacher()                     # speculative: all -1 if every env is done
-        # every env is done once its timer reaches 0 (imitation.py:42, 62-63)
-        if t >= T or int(live[t - 1]) == 0:
-            break
-    return t
+def _stepper(sim, teach, bc, success):
+    """do_rollout's per-tick craft_step_ex / craft_step_teach (include/craft.h) with the argument
+    struct built once: a tick sets only its pointers and the tick number (every buffer is one
+    do_rollout allocated and shaped itself, or the student's int32 [n] actions)."""
+    args = N.craft_step_args_t()
+    args.flags = 0                                         # no auto-reset: done envs freeze
+    if bc is not None:
+        args.behavior_clone = bc.data_ptr()
+    args.success = success.data_ptr()
+    lib = N.lib()
+    fn = lib.craft_step_teach if teach else lib.craft_step_ex
+    h, pargs, di = sim._h, ctypes.byref(args), sim.device.index
+    raw = torch._C._cuda_getCurrentRawStream
+
+    def step(t, actions, obs, ref, rec, live, labels):
+        args.actions = actions.data_ptr()
+        args.tick = t
+        args.obs = obs.data_ptr()
+        args.ref_actions = None if ref is None else ref.data_ptr()
+        args.action_record = rec.data_ptr()
+        args.any_live = live.data_ptr()
+        st = fn(h, pargs, labels.data_ptr(), raw(di)) if teach else fn(h, pargs, raw(di))
+        if st:
+            N.check(st, h, "craft_step_teach" if teach else "craft_step_ex")
+    return step
 
 
-def _lookahead_loop(sim, act, is_eval, receive, keep_obs, obs_hist, obs, success, seqs, live,
-                    ref, ref_next, bc, T, n, dev):
+def _lookahead_loop(sim, issue, receive, is_eval, refs, live, T):
     """do_rollout's loop with tick t + 1 queued before tick t's all(done) flag is read
     (see do_rollout's lookahead).  Returns the number of real ticks."""
     flags = getattr(sim, "_live_host", None)
-    if flags is None or flags.numel() < T:                 # pinned, reused across rollouts
-        flags = sim._live_host = torch.zeros(max(T, 64), dtype=torch.int32, pin_memory=True)
+    if flags is None or flags.numel() < T + 1:             # pinned, reused across rollouts
+        flags = sim._live_host = torch.zeros(max(T + 1, 64), dtype=torch.int32, pin_memory=True)
         sim._live_events = [torch.cuda.Event() for _ in range(flags.numel())]
     events = sim._live_events
-    fused = not is_eval
-    cur = {"obs": obs, "ref": ref, "ref_next": ref_next}
 
-    def issue(t):
-        """act + step of tick t on the stream, then the flag copy behind an event; returns the
-        clone of the tick's ref_actions for receive() (taken before a later tick overwrites them)."""
-        o = cur["obs"]
-        actions = act(o, t)
-        if not torch.is_tensor(actions):
-            actions = torch.as_tensor(np.asarray(actions), device=dev)
-        actions = actions.to(device=dev, dtype=torch.int32).reshape(n)
-        if keep_obs:
-            cur["obs"] = obs_hist[t + 1]
-        sim.step(actions, tick=t, autoreset=False, obs=cur["obs"], success=success,
-                 ref_actions=None if is_eval else cur["ref"], behavior_clone=bc,
-                 action_record=seqs[t], any_live=live[t:t + 1],
-                 labels=cur["ref_next"] if fused else None)
-        got = cur["ref"].clone() if (fused and receive is not None) else None
+    def queue(t):
+        issue(t)
         flags[t:t + 1].copy_(live[t:t + 1], non_blocking=True)
         events[t].record()
-        if fused:
-            cur["ref"], cur["ref_next"] = cur["ref_next"], cur["ref"]
-        return got
 
-    pending = issue(0)
+    queue(0)
     t = 0
     while True:
-        nxt = issue(t + 1) if t + 1 < T else None           # queued before the flag is read
+        if t + 1 < T:
+            queue(t + 1)                                   # queued before tick t's flag is read
         events[t].synchronize()
-        if fused and receive is not None:
-            receive(pending)                                 # tick t is real
+        if not is_eval and receive is not None:
+            receive(refs[t])                               # tick t is real
         t += 1
         if t >= T or int(flags[t - 1]) == 0:
-            break                                            # a queued tick t is discarded
-        pending = nxt
+            break                                          # a queued tick t is discarded
     return t
 
 

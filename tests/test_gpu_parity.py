@@ -584,3 +584,40 @@ def test_rollout_shape_reports_the_launched_kernel():
                       (384, (32, 384, True))):
         sim.tune_rollout(0, req)
         assert sim.rollout_shape() == want, req
+
+
+def test_rollout_graph_replay_and_eager_interleave():
+    """A craft_rollout captured into a HIP graph (torch.cuda.graph) replays correctly any number
+    of times, interleaved with eager launches of the same handle: every replay and launch equals
+    the same launch run eagerly, and the episode counters grow by one launch's env-steps each
+    time (the captured launch has its own work-unit counter, zeroed inside the graph)."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 64)
+    n, K, R = 4096, 8, 8
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    ra, rb = (torch.empty((R, n, a.n_features), dtype=torch.float32, device="cuda") for _ in range(2))
+    da, db = (torch.empty((R, n), dtype=torch.uint8, device="cuda") for _ in range(2))
+    for s in (a, b):
+        s.reset(*specs)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        b.rollout(K, seed=4, tick0=0, obs=rb, done=db)
+    for it in range(3):
+        a.rollout(K, seed=4, tick0=0, obs=ra, done=da)        # eager reference
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(ra, rb) and torch.equal(da, db), it
+        if it == 1:                                           # an eager launch on b in between
+            a.rollout(K, seed=4, tick0=K, obs=ra, done=da)
+            b.rollout(K, seed=4, tick0=K, obs=rb, done=db)
+            assert torch.equal(ra, rb) and torch.equal(da, db)
+    sa, sb = host(a.stats()), host(b.stats())
+    np.testing.assert_array_equal(sa, sb)
+    assert sb[2] == 4 * K * n                                 # env-steps: every env every tick
+    for k, v in a.get_state().items():
+        assert torch.equal(v, b.get_state()[k]), k
+    a.check()
+    b.check()

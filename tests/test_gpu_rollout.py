@@ -121,12 +121,15 @@ def test_imitation_rollout_replays_dataset(golden, gpu):
     assert len(runner._sims) == 2
 
 
-@pytest.mark.parametrize("is_eval,keep_obs", [(False, False), (True, True)])
-def test_lookahead_equals_sync_loop_full_size(gpu, is_eval, keep_obs):
+@pytest.mark.parametrize("is_eval,keep_obs,bc_rate,stop_at", [(False, False, 0.0, 6),
+                                                              (True, True, 0.0, 9),
+                                                              (False, False, 0.5, None)])
+def test_lookahead_equals_sync_loop_full_size(gpu, is_eval, keep_obs, bc_rate, stop_at):
     """Config 3/5 size (65,536 envs): the lookahead loop gives the synchronous loop's result
     bit for bit: action_seqs, success, distances, counters, every receive() call, ticks and
-    (keep_obs) every observation; a policy that stops most episodes early makes the loop end
-    before the timer, so the discarded speculative tick is exercised."""
+    (keep_obs) every observation.  With stop_at the policy answers STOP from that tick on, so the
+    loop ends before the timer and the discarded speculative tick is exercised; with cloning the
+    teacher's episodes run to the timer."""
     from psketch_amd import CraftSim
     from psketch_amd.rollout import do_rollout
     from psketch_amd.sim import sample_scenarios, synthetic_specs
@@ -137,19 +140,26 @@ def test_lookahead_equals_sync_loop_full_size(gpu, is_eval, keep_obs):
     spec = synthetic_specs(pool, 12, 12, n, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
     rng = np.random.RandomState(4)
     W = rng.randint(-3, 4, size=(4, cfg.n_features, 6))
-    bias = np.asarray([0, 1, 2, 3, 4, 6])                 # STOP is favoured: early all-done
-    bc = rng.binomial(1, 0.5, size=n)
+    bias = np.asarray([0, 1, 2, 3, 4, 0])
+    bc = rng.binomial(1, bc_rate, size=n)
+    base = torch_policy(W, bias, gpu)
+
+    def act(obs, t):
+        a = base(obs, t)
+        return torch.full_like(a, 5) if stop_at is not None and t >= stop_at else a
+
     outs = []
     for lookahead in (False, True):
         sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
         sim.load_pool(pool)
         received = []
-        info = do_rollout(sim, spec, torch_policy(W, bias, gpu), is_eval, behavior_clone=bc,
+        info = do_rollout(sim, spec, act, is_eval, behavior_clone=bc,
                           receive=lambda r: received.append(r.cpu().numpy()), keep_obs=keep_obs,
                           lookahead=lookahead)
         outs.append((info, received))
     (a, ra), (b, rb) = outs
-    assert a.ticks == b.ticks and a.ticks < cfg.max_timesteps
+    assert a.ticks == b.ticks
+    assert a.ticks == (stop_at + 1 if stop_at is not None else cfg.max_timesteps)
     for k in ("action_seqs", "n_actions", "success", "distances"):
         assert torch.equal(getattr(a, k), getattr(b, k)), k
     assert (a.num_interactions, a.num_steps) == (b.num_interactions, b.num_steps)
