@@ -600,8 +600,8 @@ def run_trainer(args):
                                                  device=dev)).cpu().tolist()
 
     # ---- per-tick split, outside the timed region: HIP events at the start and the end of the
-    # student's kernels of every tick of one more rollout; the env launch (craft_step_teach,
-    # and the flag's 4-byte copy) runs between one tick's policy end and the next one's start ----
+    # student's kernels of every tick of one more rollout; the env launch (craft_step_teach)
+    # runs between one tick's policy end and the next one's start ----
     marks = []
 
     def timed_act(obs, t):
@@ -622,13 +622,17 @@ def run_trainer(args):
     env_us = float(np.mean([marks[k][1].elapsed_time(marks[k + 1][0])
                             for k in range(min(info.ticks, len(marks) - 1))])) * 1e3
     sim.check()
+    # the tick kernel's own device duration over one more rollout (as rocprof prices it: without
+    # the dispatch gaps env_kernel above includes)
+    kname, kenvs, lanes = sim.step_shape(teach=True)
+    prof_us = profiled_kernel_us(rollout, 1, kname)
+    kernel_us = prof_us if prof_us else env_us
 
     if rank == 0:
         win = sim.params["WINDOW_WIDTH"]
         F = sim.n_features
-        kname, kenvs, lanes = sim.step_shape(teach=True)
         bps = bytes_per_env_step(sim.width, sim.height, win, F, True, 4)
-        achieved = bps * n / (env_us * 1e-6) / 1e9
+        achieved = bps * n / (kernel_us * 1e-6) / 1e9
         value = tot[0] / elapsed
         line = {
             "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
@@ -653,17 +657,23 @@ def run_trainer(args):
                        "env slot every tick", "lookahead": True,
                        "parallelism": f"env-shard x{world_size}"},
             "live_env_steps_per_s": tot[1] / elapsed,
-            "per_tick_us": {"wall": wall * 1e6, "policy": pol_us, "env_kernel": env_us,
+            "per_tick_us": {"wall": wall * 1e6, "policy": pol_us, "env": env_us,
+                            "env_kernel_device": kernel_us,
                             "host_gap": wall * 1e6 - pol_us - env_us,
                             "note": "one instrumented rollout after the timed region: HIP events "
-                                    "at the start and end of the student's kernels; env_kernel = "
-                                    "policy end to the next tick's policy start (the "
-                                    "craft_step_teach launch and the any-live flag copy)"},
+                                    "at the start and end of the student's kernels; env = policy "
+                                    "end to the next tick's policy start (the craft_step_teach "
+                                    "launch, its any-live flag stored into mapped host memory, "
+                                    "and the dispatch gaps around it); env_kernel_device = the "
+                                    "kernel's own duration"},
             "roofline": {"bound": "latency (tick prologue + BFS beside the observation stream)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": f"{kname} (craft_step_teach, {kenvs} envs, {lanes} teacher lanes)",
-                         "kernel_us": env_us, "bytes_per_env_step": bps,
+                         "kernel_us": kernel_us,
+                         "kernel_us_source": ("torch profiler device records (as rocprof)" if prof_us
+                                              else "HIP events: policy end to next policy start"),
+                         "bytes_per_env_step": bps,
                          "bytes_per_launch": bps * n, "ceiling_gbs": ceiling_gbs,
                          "frac_of_ceiling": achieved / ceiling_gbs,
                          "ceiling": f"torch zero_ of one [n, F] fp32 buffer rewritten in place, as "

@@ -291,6 +291,12 @@ typedef struct {
 } craft_step_args_t;
 int craft_step_ex(craft_sim_t* sim, const craft_step_args_t* args, void* stream);
 
+/* The device address of page-locked host memory (hipHostGetDevicePointer), e.g. for an
+ * any_live flag array the host polls after an event instead of copying each tick's flag
+ * back (the kernel's plain stores of 1 are visible to the host once the launch has
+ * completed).  CRAFT_EINVAL if `host` is not page-locked memory HIP maps. */
+int craft_host_flag_pointer(void* host, int32_t** device_out);
+
 /* craft_step_ex fused with craft_teacher on every slot's NEW state (its own task),
  * in one launch: label_out (device int32[n_envs]) receives
  * DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) of each slot

@@ -109,6 +109,7 @@ SIGNATURES = {
     "craft_sim_destroy": (_i32, [_vp]),
     "craft_sim_last_error": (ctypes.c_char_p, [_vp]),
     "craft_strerror": (ctypes.c_char_p, [_i32]),
+    "craft_host_flag_pointer": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "craft_sim_info": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32),
                               ctypes.POINTER(_i32)]),
     "craft_sim_check": (_i32, [_vp, ctypes.POINTER(_i64), _vp]),

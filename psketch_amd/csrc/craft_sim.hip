@@ -327,6 +327,18 @@ const char* craft_strerror(int status) {
   }
 }
 
+int craft_host_flag_pointer(void* host, int32_t** device_out) {
+  if (!host || !device_out) return CRAFT_EINVAL;
+  *device_out = nullptr;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, host, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    return CRAFT_EINVAL;                    // not page-locked host memory HIP knows
+  }
+  *device_out = static_cast<int32_t*>(d);
+  return CRAFT_OK;
+}
+
 int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int64_t env_id_base,
                      int32_t pool_capacity, craft_sim_t** out) {
   if (!cfg || !out || n_envs <= 0 || pool_capacity <= 0 || pool_capacity > (1 << 24) || env_id_base < 0)

@@ -12,8 +12,9 @@ a kernel on the current stream:
                           and an any-env-still-running flag (:42)
 
 The student sees the features as a device tensor and returns device actions;
-nothing crosses PCIe inside the loop except the all(done) test (one int32 per
-tick, imitation.py:42).  After the loop, `distances` (imitation.py:79-91) come
+nothing crosses PCIe inside the loop except the all(done) test (imitation.py:42):
+the step kernels store each tick's any-live flag straight into page-locked host
+memory, which the host reads once the tick's event has completed.  After the loop, `distances` (imitation.py:79-91) come
 from the same teacher kernel: failed get-tasks are reset to their initial grid
 at their final position and find_closest_resources' length is read back.
 """
@@ -78,9 +79,8 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
       (craft_step_teach: the next tick's ref_actions, in the same launch);
       False runs craft_teacher on a side stream, overlapping the student.
     lookahead: the all(done) test of tick t (imitation.py:42) no longer blocks the
-      host before tick t + 1 is queued: the any-live flag is copied to pinned host
-      memory behind an event, tick t + 1 (act and step) is queued, and only then is the
-      flag read.  When tick t ended every episode the queued tick is discarded: its step
+      host before tick t + 1 is queued: tick t + 1 (act and step) is queued behind tick
+      t's event, and only then is tick t's any-live flag read.  When tick t ended every episode the queued tick is discarded: its step
       is a no-op on frozen envs (no state, counter, success or action-record change that
       the result keeps), but act was called once more than the reference calls it, so
       lookahead is for side-effect-free students (a fixed or deterministic policy);
@@ -100,7 +100,11 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     sim.reset(*spec, obs=obs)
     success = torch.zeros(n, dtype=torch.int8, device=dev)
     seqs = torch.full((T, n), -1, dtype=torch.int32, device=dev)
-    live = torch.zeros(T + 1, dtype=torch.int32, device=dev)  # 1: some env still running after tick t
+    # any-live flags (1: some env still running after tick t), one per tick: page-locked host
+    # memory the kernel stores into directly where HIP maps it (read after the tick's event),
+    # else a device array copied back per tick
+    flags, flag_dev, events = _live_flags(sim, T)
+    live = None if flag_dev else torch.zeros(T + 1, dtype=torch.int32, device=dev)
     # ref_actions of every tick: tick t reads refs[t] and (fused) labels refs[t + 1]; receive()
     # gets the row itself (no copy), which no later tick or rollout overwrites
     refs = None if is_eval else torch.empty((T + 1, n), dtype=torch.int32, device=dev)
@@ -139,7 +143,8 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
 
     def issue(t):
         """Tick t on the stream: the student's act, then one step launch (behaviour cloning, the
-        action record, the any-live flag and, fused, the next tick's labels)."""
+        action record, the any-live flag and, fused, the next tick's labels), then the flag's
+        event (after the flag's copy to the host where it is not mapped)."""
         actions = act(cur["obs"], t)
         if not torch.is_tensor(actions):
             actions = torch.as_tensor(np.asarray(actions), device=dev)
@@ -148,10 +153,13 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
             main.wait_event(labels_ready)
         if keep_obs:
             cur["obs"] = obs_hist[t + 1]
-        step(t, actions, cur["obs"], None if is_eval else refs[t], seqs[t], live[t:t + 1],
-             refs[t + 1] if fused else None)
+        step(t, actions, cur["obs"], None if is_eval else refs[t], seqs[t],
+             flag_dev + 4 * t if flag_dev else live[t].data_ptr(), refs[t + 1] if fused else None)
         if side is not None and t + 1 < T:
             launch_teacher(t + 1)                # speculative: all -1 if every env is done
+        if not flag_dev:
+            flags[t:t + 1].copy_(live[t:t + 1], non_blocking=True)
+        events[t].record()
 
     if not is_eval:
         if fused_teacher:
@@ -159,18 +167,22 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
         else:
             launch_teacher(0)
     t_loop = time.perf_counter()
-    if lookahead:
-        t = _lookahead_loop(sim, issue, receive, is_eval, refs, live, T)
-    else:
-        t = 0
-        while True:
+    # every env is done once its timer reaches 0 (imitation.py:42, 62-63): tick t's flag is read
+    # after its event; with lookahead, tick t + 1 is queued first (and discarded if every
+    # episode ended at tick t)
+    issue(0)
+    t = 0
+    while True:
+        if lookahead and t + 1 < T:
+            issue(t + 1)
+        events[t].synchronize()
+        if not is_eval and receive is not None:
+            receive(refs[t])                     # tick t is real
+        t += 1
+        if t >= T or int(flags[t - 1]) == 0:
+            break
+        if not lookahead:
             issue(t)
-            if not is_eval and receive is not None:
-                receive(refs[t])
-            t += 1
-            # every env is done once its timer reaches 0 (imitation.py:42, 62-63)
-            if t >= T or int(live[t - 1]) == 0:
-                break
     if side is not None:
         main.wait_stream(side)
     t_end_loop = time.perf_counter()
@@ -192,45 +204,33 @@ def _stepper(sim, teach, bc, success):
     h, pargs, di = sim._h, ctypes.byref(args), sim.device.index
     raw = torch._C._cuda_getCurrentRawStream
 
-    def step(t, actions, obs, ref, rec, live, labels):
+    def step(t, actions, obs, ref, rec, live_ptr, labels):
         args.actions = actions.data_ptr()
         args.tick = t
         args.obs = obs.data_ptr()
         args.ref_actions = None if ref is None else ref.data_ptr()
         args.action_record = rec.data_ptr()
-        args.any_live = live.data_ptr()
+        args.any_live = live_ptr
         st = fn(h, pargs, labels.data_ptr(), raw(di)) if teach else fn(h, pargs, raw(di))
         if st:
             N.check(st, h, "craft_step_teach" if teach else "craft_step_ex")
     return step
 
 
-def _lookahead_loop(sim, issue, receive, is_eval, refs, live, T):
-    """do_rollout's loop with tick t + 1 queued before tick t's all(done) flag is read
-    (see do_rollout's lookahead).  Returns the number of real ticks."""
+def _live_flags(sim, T):
+    """The per-tick any-live flags of do_rollout: a page-locked host int32 array (zeroed here,
+    reused across rollouts: the previous rollout's ticks have completed when it returned), its
+    device address (craft_host_flag_pointer) or 0 where HIP does not map it, and one event per
+    tick."""
     flags = getattr(sim, "_live_host", None)
-    if flags is None or flags.numel() < T + 1:             # pinned, reused across rollouts
+    if flags is None or flags.numel() < T + 1:
         flags = sim._live_host = torch.zeros(max(T + 1, 64), dtype=torch.int32, pin_memory=True)
         sim._live_events = [torch.cuda.Event() for _ in range(flags.numel())]
-    events = sim._live_events
-
-    def queue(t):
-        issue(t)
-        flags[t:t + 1].copy_(live[t:t + 1], non_blocking=True)
-        events[t].record()
-
-    queue(0)
-    t = 0
-    while True:
-        if t + 1 < T:
-            queue(t + 1)                                   # queued before tick t's flag is read
-        events[t].synchronize()
-        if not is_eval and receive is not None:
-            receive(refs[t])                               # tick t is real
-        t += 1
-        if t >= T or int(flags[t - 1]) == 0:
-            break                                          # a queued tick t is discarded
-    return t
+        p = ctypes.c_void_p()
+        ok = N.lib().craft_host_flag_pointer(flags.data_ptr(), ctypes.byref(p)) == 0
+        sim._live_dev = p.value if ok and p.value else 0
+    flags[:T + 1].zero_()
+    return flags, sim._live_dev, sim._live_events
 
 
 def _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot_ids, timing,

@@ -168,3 +168,16 @@ def test_lookahead_equals_sync_loop_full_size(gpu, is_eval, keep_obs, bc_rate, s
         assert np.array_equal(x, y)
     if keep_obs:
         assert torch.equal(a.obs, b.obs)
+    assert sim._live_dev != 0                  # the flags were stored into mapped host memory
+
+
+def test_host_flag_pointer(gpu):
+    """craft_host_flag_pointer maps torch's page-locked memory (the any-live flags) and refuses
+    pageable memory."""
+    import ctypes
+    from psketch_amd import _native as N
+    p = ctypes.c_void_p()
+    pinned = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+    assert N.lib().craft_host_flag_pointer(pinned.data_ptr(), ctypes.byref(p)) == 0 and p.value
+    plain = torch.zeros(8, dtype=torch.int32)
+    assert N.lib().craft_host_flag_pointer(plain.data_ptr(), ctypes.byref(p)) == N.EINVAL
