@@ -9,15 +9,6 @@ namespace craft {
 
 typedef unsigned int obs_vec __attribute__((ext_vector_type(4)));
 
-// Kind id at (cx, cy) of an LDS grid row as a one-hot bit, 0 outside the grid
-// (pad_slice's zero padding, misc/array.py:3-25).
-__device__ __forceinline__ uint32_t cell_bit(const uint8_t* g, int W, int H, int cx, int cy) {
-  const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-  const int xc = min(max(cx, 0), W - 1), yc = min(max(cy, 0), H - 1);
-  const int k = g[xc * H + yc];
-  return ok ? (1u << k) : 0u;
-}
-
 // 16 bytes of output from the tile's u8 feature rows: 4 fp32 (v_cvt_f32_ubyte),
 // 8 bf16 (the high half of the exact fp32 value of a byte) or 16 u8.
 template <int FMT>
@@ -90,87 +81,29 @@ __device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t en
   }
 }
 
-// Phase D: all threads scatter the non-zero bytes of each env's features() row
-// into the zeroed u8 rows s_obs[TILE][F]: local one-hots, block-max-pooled
-// one-hots, inventory counts, dir one-hot.  s_agent[e] = x | y<<8 | dir<<16 | 1<<24
-// for a live env (0 = skip).
-template <int WIN, int TILE, int NTHR = kThreads>
-__device__ __forceinline__ void scatter_features(const SimView& v, const uint8_t* s_grid,
-                                                 const uint8_t* s_inv, const uint32_t* s_agent,
-                                                 uint8_t* s_obs, int nE, int tid) {
-  constexpr int kParts = NTHR / TILE;            // threads per env
-  static_assert(kParts >= 2, "the scatter needs at least two threads per env");
-  const int F = v.F;
-  {
-    const int e = tid % TILE, part = tid / TILE;
-    const uint32_t ag = s_agent[e];
-    if (e < nE && (ag >> 24)) {
-      const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
-      const uint8_t* g = s_grid + e * v.GS;
-      uint8_t* row = s_obs + e * F;
-      const int W = v.W, H = v.H, K = v.K;
-      constexpr int W2 = WIN * WIN;
-      const int L = W2 * K;
-      if (part == 0) {
-        constexpr int hw = WIN / 2;
-#pragma unroll
-        for (int i = 0; i < WIN; ++i)
-#pragma unroll
-          for (int j = 0; j < WIN; ++j) {
-            const int cx = x - hw + i, cy = y - hw + j;
-            if ((unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H) {
-              const int k = g[cx * H + cy];
-              if (k) row[(i * WIN + j) * K + k] = 1;                   // local one-hot
-            }
-          }
-        const uint8_t* iv = s_inv + e * kInvStride;
-        for (int k = 0; k < K; ++k) row[2 * L + k] = iv[k];           // inventory counts
-        row[2 * L + K + dir] = 1;                                      // dir one-hot
-      } else {
-        constexpr int bh = W2 / 2;
-#pragma unroll
-        for (int j = 0; j < (W2 + kParts - 2) / (kParts - 1); ++j) {
-          const int b = part - 1 + (kParts - 1) * j;
-          if (b >= W2) break;
-          const int bi = b / WIN, bj = b - bi * WIN;
-          const int x0 = x - bh + bi * WIN, y0 = y - bh + bj * WIN;
-          uint32_t msk = 0;
-          if (x0 < W && x0 + WIN > 0 && y0 < H && y0 + WIN > 0) {
-#pragma unroll
-            for (int ii = 0; ii < WIN; ++ii)
-#pragma unroll
-              for (int jj = 0; jj < WIN; ++jj) msk |= cell_bit(g, W, H, x0 + ii, y0 + jj);
-          }
-          msk &= ~1u;                                                  // kind 0 = empty
-          uint8_t* brow = row + L + b * K;
-          while (msk) {                                                // block-max-pooled one-hot
-            brow[__ffs(msk) - 1] = 1;
-            msk &= msk - 1;
-          }
-        }
-      }
-    }
-  }
-}
-
-// Phase D for one env, split over P lanes of the rollout kernel's producer wave
-// (right after the envs' transitions, no workgroup barrier): the features() row
-// (craft.py:296-330) is WIN + 1 items, item 0 = local one-hot + inventory + dir
-// one-hot, item 1 + bi = the pooled blocks of block row bi, and part p of the env
-// writes items p, p + P, ...  `ag` = x | y<<8 | dir<<16; `row` is zeroed.  A
-// block row is built column by column (each of its WIN columns ORs the kind bits
-// of its cells into the WIN blocks it crosses); columns or cells outside the
-// grid are skipped (pad_slice's zero padding, misc/array.py:3-25).
+// Phase D for one env, split over P lanes (right after the envs' transitions, no
+// workgroup barrier): the features() row (craft.py:296-330) as 1 + nc work units,
+// unit 0 = local one-hot + inventory + dir one-hot, unit 1 + c = grid column c of
+// the pooled window (the W2 x W2 cells around the agent that lie inside the grid),
+// and part p of the env does units p, p + P, ...  `ag` = x | y<<8 | dir<<16; `row`
+// is zeroed.  The pooled blocks tile the window without overlap, so each in-grid
+// cell sets the one-hot byte of its kind in its own block: a block-max-pooled
+// one-hot costs one read per grid cell, not one per block cell (cells outside the
+// grid are pad_slice's zero padding, misc/array.py:3-25, and set nothing).
 template <int WIN, int P>
 __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t* g, const uint8_t* iv,
                                                  uint32_t ag, uint8_t* row, int part) {
   const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
   const int W = v.W, H = v.H, K = v.K;
   constexpr int W2 = WIN * WIN, hw = WIN / 2, bh = W2 / 2;
+  constexpr int NR = W2 < CRAFT_MAX_DIM ? W2 : CRAFT_MAX_DIM;       // window rows inside a grid
   const int L = W2 * K;
+  const int cxa = max(x - bh, 0), cxb = min(x - bh + W2 - 1, W - 1);
+  const int cya = max(y - bh, 0), cyb = min(y - bh + W2 - 1, H - 1);
+  const int nc = cxb - cxa + 1;
 #pragma unroll 1
-  for (int item = part; item <= WIN; item += P) {
-    if (item == 0) {
+  for (int unit = part; unit <= nc; unit += P) {
+    if (unit == 0) {
       // every read is unconditional (clamped index, result masked), so the compiler issues
       // them back to back instead of one LDS round trip per predicated cell
       int kk[WIN * WIN];
@@ -207,36 +140,36 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
       }
       row[2 * L + K + dir] = 1;                                     // dir one-hot
     } else {
-      const int bi = item - 1;                                      // block-max-pooled one-hots
-      uint32_t m[WIN];
+      // block-max-pooled one-hots: column cx of the window, block row bi; its cells' reads
+      // are issued back to back (clamped, masked), then each non-empty cell sets its byte
+      const int cx = cxa + unit - 1;
+      const int bi = (cx - x + bh) / WIN;
+      const uint8_t* col = g + cx * H;
+      uint8_t* brow = row + L + bi * WIN * K;
+      int kk[NR];
 #pragma unroll
-      for (int bj = 0; bj < WIN; ++bj) m[bj] = 0;
-      const int x0 = x - bh + bi * WIN;
+      for (int j = 0; j < NR; ++j) kk[j] = col[min(cya + j, H - 1)];
 #pragma unroll
-      for (int ii = 0; ii < WIN; ++ii) {
-        const int cx = x0 + ii;
-        const bool okx = (unsigned)cx < (unsigned)W;
-        const uint8_t* col = g + min(max(cx, 0), W - 1) * H;
-#pragma unroll
-        for (int bj = 0; bj < WIN; ++bj)
-#pragma unroll
-          for (int jj = 0; jj < WIN; ++jj) {
-            const int cy = y - bh + bj * WIN + jj;
-            const uint32_t k = col[min(max(cy, 0), H - 1)];          // unconditional read
-            m[bj] |= (okx && (unsigned)cy < (unsigned)H) ? (1u << k) : 0u;
-          }
-      }
-#pragma unroll
-      for (int bj = 0; bj < WIN; ++bj) {
-        uint32_t msk = m[bj] & ~1u;                                 // kind 0 = empty
-        uint8_t* brow = row + L + (bi * WIN + bj) * K;
-        while (msk) {
-          brow[__ffs(msk) - 1] = 1;
-          msk &= msk - 1;
-        }
+      for (int j = 0; j < NR; ++j) {
+        const int cy = cya + j;
+        if (cy <= cyb && kk[j]) brow[((cy - y + bh) / WIN) * K + kk[j]] = 1;   // kind 0 = empty
       }
     }
   }
+}
+
+// Phase D: all threads scatter the non-zero bytes of each env's features() row
+// into the zeroed u8 rows s_obs[TILE][F] (scatter_env_part, NTHR / TILE threads per
+// env).  s_agent[e] = x | y<<8 | dir<<16 | 1<<24 for a live env (0 = skip).
+template <int WIN, int TILE, int NTHR = kThreads>
+__device__ __forceinline__ void scatter_features(const SimView& v, const uint8_t* s_grid,
+                                                 const uint8_t* s_inv, const uint32_t* s_agent,
+                                                 uint8_t* s_obs, int nE, int tid) {
+  constexpr int kParts = NTHR / TILE;            // threads per env
+  const int e = tid % TILE, part = tid / TILE;
+  const uint32_t ag = s_agent[e];
+  if (e < nE && (ag >> 24))
+    scatter_env_part<WIN, kParts>(v, s_grid + e * v.GS, s_inv + e * kInvStride, ag, s_obs + e * v.F, part);
 }
 
 }  // namespace craft

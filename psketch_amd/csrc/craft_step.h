@@ -344,7 +344,7 @@ void step_kernel(SimView v, TileArgs a) {
         if (k >= 2) seq_wait(sq, (uint32_t)(k & ~1));                 // use u - 1 streamed, cleared
         uint8_t* buf = smem + lay.buf0 + b * lay.buf;
         const int e = k * SUB + e_in;
-        if (e_in < nEs && part <= WIN) {
+        if (e_in < nEs) {
           const uint32_t ag = s_agent[e];
           if (ag >> 24) scatter_env_part<WIN, P>(v, s_grid + e * GS, s_inv + e * kInvStride, ag, buf + e_in * F, part);
         }
@@ -352,7 +352,7 @@ void step_kernel(SimView v, TileArgs a) {
         if (k == 0 && v.stamps) {     // the first scatter again (idempotent): warm-code timing
           lds_release();
           STEP_STAMP2(2);
-          if (e_in < nEs && part <= WIN) {
+          if (e_in < nEs) {
             const uint32_t ag = s_agent[e];
             if (ag >> 24) scatter_env_part<WIN, P>(v, s_grid + e * GS, s_inv + e * kInvStride, ag, buf + e_in * F, part);
           }

@@ -562,7 +562,22 @@ def test_rollout_fast_path_revalidates_resized_rings():
     ring.resize_(4, n // 2, sim.n_features)
     with pytest.raises(ValueError):
         sim.rollout(3, tick0=6, obs=ring, done=done)
+    # re-strided in place to a non-contiguous view of the same storage: refused
+    ring2 = torch.empty((4, n, sim.n_features), dtype=torch.float32, device="cuda")
+    sim.rollout(3, tick0=6, obs=ring2, done=done)
+    ring2.as_strided_((4, n, sim.n_features), (n * sim.n_features, 1, n))
+    with pytest.raises(ValueError):
+        sim.rollout(3, tick0=9, obs=ring2, done=done)
+    # the cache holds no reference: a dropped ring is freed
+    import weakref
+    ring3 = torch.empty((4, n, sim.n_features), dtype=torch.float32, device="cuda")
+    sim.rollout(3, tick0=9, obs=ring3, done=done)
+    r = weakref.ref(ring3)
+    del ring3
+    assert r() is None
     sim.check()
+    sim.close()
+    assert sim._rollout_cache is None
 
 
 def test_rollout_shape_reports_the_launched_kernel():

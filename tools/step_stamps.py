@@ -26,7 +26,7 @@ import __graft_entry__ as ge  # noqa: E402
 DIAG = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_diag.so")
 
 
-def build():
+def build(stamped=("craft_sim", "craft_step")):
     ge.build()
     obj = os.path.join(REPO, "psketch_amd", "lib", "obj")
     dobj = os.path.join(REPO, "psketch_amd", "lib", "obj_diag")
@@ -34,7 +34,7 @@ def build():
     objs = []
     for src in ge.SOURCES:
         base = os.path.splitext(src)[0]
-        if base in ("craft_sim", "craft_step"):
+        if base in stamped:
             o = os.path.join(dobj, base + ".o")
             subprocess.check_call([ge.HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                                    "-DCRAFT_STAMPS", "-c", os.path.join(ge.CSRC, src), "-o", o])
