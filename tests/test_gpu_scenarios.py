@@ -93,3 +93,38 @@ def test_generated_pool_rollout_matches_oracle(gpu, oracle_mod):
         assert rc == 0
         assert np.array_equal(obs.cpu().numpy(), oobs), t
     sim.check()
+
+
+@pytest.mark.parametrize("n,kernel", [(65536, 0), (4096, 0), (40000, 1)])
+def test_generated_pool_teacher_labels_match_oracle(gpu, oracle_mod, n, kernel):
+    """Teacher labels on device-generated worlds (craft_pool_generate marks their free cells
+    connected, which the teacher's reachability test uses): the fused labels of craft_step_teach
+    (two-tile at 65,536 / one-tile at 4096 and when forced) and craft_teacher against the literal
+    BFS oracle on every tick of a sample."""
+    from psketch_amd.sim import synthetic_specs
+    params, cb, prims, ws = gen_args("craft_medium_12x12")
+    P = 1024
+    sim = CraftSim("craft_medium_12x12", n_envs=n, device=0, pool_capacity=P)
+    sim.tune_teach(kernel)
+    sim.generate_pool(P, seed=21)
+    grids, _, _ = oracle_mod.generate_scenarios(12, 12, cb.index["boundary"], prims,
+                                                params["N_PRIMITIVES"], ws, P, 21)
+    tasks = [t.id for t in sim.task_manager.dataset_tasks()]
+    specs = synthetic_specs(grids, 12, 12, n, 0, seed=4, task_ids=tasks)
+    sim.reset(*specs)
+    o = oracle_mod.Oracle(sim.config, grids)
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    sep = torch.empty(n, dtype=torch.int32, device="cuda")
+    ids = np.random.RandomState(n).choice(n, 256, replace=False)
+    for t in range(12):
+        sim.step(seed=9, tick=t, labels=lab)
+        sim.teacher(action_out=sep)
+        assert torch.equal(lab, sep), t
+        st = {k: v.cpu().numpy() for k, v in sim.get_state(fields=("agent", "inventory", "grid")).items()}
+        got = lab.cpu().numpy()
+        for i in ids:
+            x, y, d, _ = st["agent"][i]
+            env = o.env(st["grid"][i], x, y, d, st["inventory"][i])
+            rc, act = o.teacher(env, int(specs[4][i]))
+            assert rc == 0 and act == got[i], (t, i)
+    sim.check()
