@@ -109,6 +109,9 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=8.0,
                    help="wall seconds of each cpu_baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-kernel-profiler", action="store_true",
+                   help="price one-tick kernels by HIP events only (for runs under rocprofv3, "
+                        "whose tracer the torch profiler would share)")
     p.add_argument("--obs-format", choices=("f32", "bf16", "u8"), default="f32",
                    help="observation element type (the same exact values in each; the metric's "
                         "line is f32, what students/imitation.py:73 feeds the model)")
@@ -252,6 +255,21 @@ def fill_ceiling(bufs, reps=8):
 
 
 
+def pmc_traffic(args, workload, k):
+    """HBM bytes per launch of this workload's dominant kernel from the PMC passes
+    (tools/profile.sh + tools/pmc_summary.py -> profiles/pmc_traffic.json), or None."""
+    tpath = args.traffic or os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(tpath) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for e in (tj if isinstance(tj, list) else [tj]):
+        if e.get("workload") == workload and e.get("ticks_per_launch", 1) == k:
+            return e.get("hbm_bytes_per_launch")
+    return None
+
+
 def profiled_kernel_us(fn, m, name):
     """Mean device duration (µs) of the kernels whose name contains `name` over m calls of fn(),
     from the torch profiler's device activity (roctracer on ROCm: the same launch records as
@@ -379,7 +397,7 @@ def run(args):
     # one launch per tick (craft_step / craft_step_teach): price the kernel's own duration (the
     # profiler's device records, as rocprof reports them), not launches plus dispatch gaps
     prof_us = None
-    if K == 1:
+    if K == 1 and not args.no_kernel_profiler:
         if teacher and args.teacher_mode == "fused":
             pname = {"tile_kernel": "tile_kernel", "tick2_kernel": "tick2_kernel",
                      "step_kernel": "step_kernel"}[sim.step_shape(teach=True)[0]]
@@ -424,18 +442,7 @@ def run(args):
             workload += f"_obs_{sim.obs_format}"
         if teacher:
             workload += "_" + args.teacher_mode
-        traffic = None
-        tpath = args.traffic or os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tpath):
-            try:
-                with open(tpath) as f:
-                    tj = json.load(f)
-                entries = tj if isinstance(tj, list) else [tj]
-                for e in entries:
-                    if e.get("workload") == workload and e.get("ticks_per_launch", K) == k_eff:
-                        traffic = e.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        traffic = pmc_traffic(args, workload, k_eff)
         if teacher:
             bound = ("latency: the tick's prologue plus the BFS beside the observation stream "
                      "(store floor of the tick's bytes at the in-situ ceiling below)")
@@ -625,7 +632,7 @@ def run_trainer(args):
     # the tick kernel's own device duration over one more rollout (as rocprof prices it: without
     # the dispatch gaps env_kernel above includes)
     kname, kenvs, lanes = sim.step_shape(teach=True)
-    prof_us = profiled_kernel_us(rollout, 1, kname)
+    prof_us = None if args.no_kernel_profiler else profiled_kernel_us(rollout, 1, kname)
     kernel_us = prof_us if prof_us else env_us
 
     if rank == 0:
@@ -633,6 +640,7 @@ def run_trainer(args):
         F = sim.n_features
         bps = bytes_per_env_step(sim.width, sim.height, win, F, True, 4)
         achieved = bps * n / (kernel_us * 1e-6) / 1e9
+        workload = f"{args.world}_w{win}_B{n}_trainer_closed_loop_train_fused_teacher"
         value = tot[0] / elapsed
         line = {
             "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
@@ -649,7 +657,7 @@ def run_trainer(args):
             "data": "synthetic: 1024 make_data.sample_scenario worlds (RandomState(123)), per-env "
                     "init keyed by global id, a fixed integer-weight linear student, behaviour "
                     "cloning mix 0.5",
-            "config": {"workload": f"{args.world}_w{win}_B{n}_trainer_closed_loop_train_fused_teacher",
+            "config": {"workload": workload,
                        "world": args.world, "envs_per_gpu": n, "global_batch": n * world_size,
                        "window": win, "n_features": F, "max_timesteps": sim.config.max_timesteps,
                        "rollouts": args.steps, "ticks": tot[2], "step": "one do_rollout "
@@ -668,7 +676,7 @@ def run_trainer(args):
                                     "kernel's own duration"},
             "roofline": {"bound": "latency (tick prologue + BFS beside the observation stream)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, workload, 1),
                          "kernel": f"{kname} (craft_step_teach, {kenvs} envs, {lanes} teacher lanes)",
                          "kernel_us": kernel_us,
                          "kernel_us_source": ("torch profiler device records (as rocprof)" if prof_us

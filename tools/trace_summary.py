@@ -1,5 +1,5 @@
 """Per-launch durations of the bench kernel from rocprofv3 kernel traces
-(tools/profile_round.sh), without the first launch of each run (bench.py's
+(tools/profile.sh), without the first launch of each run (bench.py's
 --warmup 5: a 5-tick launch), so the average is over the launches of the timed
 tick count only.  usage: python tools/trace_summary.py gpurun_out/<tag> profiles/<round>"""
 import csv, json, os, sys
