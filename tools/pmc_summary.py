@@ -25,6 +25,10 @@ def main(src, dst):
     stats = list(csv.DictReader(open(stats_csv)))
     name = max(stats, key=lambda r: float(r["TotalDurationNs"]))["Name"]
     top = next(r for r in stats if r["Name"] == name)
+    # per-launch durations from the trace: the first launch is the warmup's when it ran fewer ticks
+    trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            for r in csv.DictReader(open(trace_csv)) if r["Kernel_Name"] == name]
     roof = line["roofline"]
     k = roof.get("ticks_per_launch", 1)
     per = {}
@@ -38,6 +42,7 @@ def main(src, dst):
     entry = {
         "workload": line["config"]["workload"], "ticks_per_launch": k, "kernel": name,
         "rocprof_calls": int(top["Calls"]), "rocprof_avg_us": float(top["AverageNs"]) / 1e3,
+        "rocprof_avg_us_after_first": sum(durs[1:]) / max(1, len(durs) - 1),
         "bench_kernel_us": roof.get("kernel_us"), "launches_counted": min(n_f, n_w),
         "fetch_size_kib_raw": fetch_kib, "write_size_kib_raw": write_kib,
         "hbm_read_bytes_per_launch": 2 * fetch_kib * 1024,
