@@ -79,6 +79,10 @@ def parse(argv=None):
                         "trainer: configs[2]/[4] closed loop, psketch_amd.rollout.do_rollout "
                         "(train mode, fused teacher labels, a fixed on-device student); "
                         "--steps counts rollouts")
+    p.add_argument("--rollout-graph", type=int, default=0,
+                   help="trainer workload: ticks per captured HIP graph in do_rollout (0 = the "
+                        "eager lookahead loop; 8 measured the same, 78.9 against 76-79 us per "
+                        "tick: the loop is bound by the kernels and their dispatch gaps)")
     p.add_argument("--teacher-mode", choices=("fused", "separate"), default="fused",
                    help="teacher workload: one craft_step_teach launch per tick, or craft_teacher "
                         "then craft_step")
@@ -583,7 +587,7 @@ def run_trainer(args):
     def rollout():
         received.clear()
         return do_rollout(sim, spec_d, act, False, behavior_clone=bc_d, receive=receive,
-                          lookahead=True)
+                          lookahead=True, graph=args.rollout_graph)
 
     for _ in range(args.warmup):
         rollout()
@@ -632,7 +636,9 @@ def run_trainer(args):
     # the tick kernel's own device duration over one more rollout (as rocprof prices it: without
     # the dispatch gaps env_kernel above includes)
     kname, kenvs, lanes = sim.step_shape(teach=True)
-    prof_us = None if args.no_kernel_profiler else profiled_kernel_us(rollout, 1, kname)
+    prof_us = None if args.no_kernel_profiler else profiled_kernel_us(
+        lambda: do_rollout(sim, spec_d, act, False, behavior_clone=bc_d, receive=receive,
+                           lookahead=True), 1, kname)
     kernel_us = prof_us if prof_us else env_us
 
     if rank == 0:
@@ -663,17 +669,20 @@ def run_trainer(args):
                        "rollouts": args.steps, "ticks": tot[2], "step": "one do_rollout "
                        "(ticks until every episode has ended, <= max_timesteps); value counts every "
                        "env slot every tick", "lookahead": True,
+                       "rollout_graph_ticks": args.rollout_graph,
                        "parallelism": f"env-shard x{world_size}"},
             "live_env_steps_per_s": tot[1] / elapsed,
-            "per_tick_us": {"wall": wall * 1e6, "policy": pol_us, "env": env_us,
+            "per_tick_us": {"timed_wall": elapsed * 1e6 / max(1, tot[2] // world_size),
+                            "eager_wall": wall * 1e6, "policy": pol_us, "env": env_us,
                             "env_kernel_device": kernel_us,
                             "host_gap": wall * 1e6 - pol_us - env_us,
-                            "note": "one instrumented rollout after the timed region: HIP events "
-                                    "at the start and end of the student's kernels; env = policy "
-                                    "end to the next tick's policy start (the craft_step_teach "
-                                    "launch, its any-live flag stored into mapped host memory, "
-                                    "and the dispatch gaps around it); env_kernel_device = the "
-                                    "kernel's own duration"},
+                            "note": "timed_wall: the timed region per tick; the rest from one "
+                                    "instrumented eager (lookahead, no graph) rollout after it: "
+                                    "HIP events at the start and end of the student's kernels; "
+                                    "env = policy end to the next tick's policy start (the "
+                                    "craft_step_teach launch, its any-live flag stored into mapped "
+                                    "host memory, and the dispatch gaps around it); "
+                                    "env_kernel_device = the kernel's own duration"},
             "roofline": {"bound": "latency (tick prologue + BFS beside the observation stream)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, workload, 1),

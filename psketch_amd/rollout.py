@@ -62,7 +62,7 @@ class RolloutInfo:
 
 
 def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_obs=False,
-               timing=None, fused_teacher=True, lookahead=False):
+               timing=None, fused_teacher=True, lookahead=False, graph=0):
     """One rollout of sim.n_envs episodes.
 
     spec: (scenario, x, y, dir, task), each n_envs ints (device or host).
@@ -86,7 +86,20 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
       lookahead is for side-effect-free students (a fixed or deterministic policy);
       receive() is still called exactly once per real tick.  Needs is_eval or the fused
       teacher.
+    graph: G > 0 runs the ticks as HIP graphs of G ticks each (act + step per tick, captured
+      with torch.cuda.graph on the first call for this simulator and this `act`, replayed by
+      later calls), so the per-tick host work (the student's launches, the step's ctypes call)
+      leaves the loop.  The conditions of lookahead apply, and more: act only queues device work
+      on the current stream, with fixed shapes and no host synchronisation, and its device
+      inputs stay where they were at capture (weights may change in place).  Chunk c + 1 is
+      queued before chunk c's flags are read; ticks after the one that ended every episode are
+      no-ops and are discarded.  The rollout's buffers are the simulator's own: the results are
+      copies, and receive() is called once per real tick after the loop, in tick order, with
+      rows of a copy of the labels.  Not with keep_obs.
     """
+    if graph:
+        return _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, timing,
+                              fused_teacher, int(graph))
     t_start = time.perf_counter()
     n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
     if T <= 0:
@@ -108,15 +121,7 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     # ref_actions of every tick: tick t reads refs[t] and (fused) labels refs[t + 1]; receive()
     # gets the row itself (no copy), which no later tick or rollout overwrites
     refs = None if is_eval else torch.empty((T + 1, n), dtype=torch.int32, device=dev)
-    bc = None
-    if not is_eval:
-        if behavior_clone is None:
-            raise ValueError("behavior_clone is required when not is_eval")
-        bc = torch.as_tensor(np.asarray(behavior_clone) if not torch.is_tensor(behavior_clone)
-                             else behavior_clone, device=dev)
-        if bc.numel() != n:
-            raise ValueError(f"behavior_clone has {bc.numel()} entries, expected {n}")
-        bc = (bc.reshape(n) != 0).to(torch.uint8).contiguous()
+    bc = None if is_eval else _bc_mask(behavior_clone, n, dev)
     fused = not is_eval and fused_teacher
     if lookahead and not is_eval and not fused_teacher:
         raise ValueError("lookahead needs is_eval or fused_teacher")
@@ -215,6 +220,99 @@ def _stepper(sim, teach, bc, success):
         if st:
             N.check(st, h, "craft_step_teach" if teach else "craft_step_ex")
     return step
+
+
+def _bc_mask(behavior_clone, n, dev):
+    if behavior_clone is None:
+        raise ValueError("behavior_clone is required when not is_eval")
+    bc = torch.as_tensor(np.asarray(behavior_clone) if not torch.is_tensor(behavior_clone)
+                         else behavior_clone, device=dev)
+    if bc.numel() != n:
+        raise ValueError(f"behavior_clone has {bc.numel()} entries, expected {n}")
+    return (bc.reshape(n) != 0).to(torch.uint8).contiguous()
+
+
+def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, timing,
+                   fused_teacher, G):
+    """do_rollout(graph=G): see do_rollout."""
+    t_start = time.perf_counter()
+    n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
+    if keep_obs:
+        raise ValueError("graph mode does not keep observations (keep_obs)")
+    if not is_eval and not fused_teacher:
+        raise ValueError("graph mode needs is_eval or fused_teacher")
+    if G < 1:
+        raise ValueError("graph: ticks per graph must be positive")
+    spec = [sim._i32(a, n) for a in spec]
+    task = spec[4]
+    flags, flag_dev, events = _live_flags(sim, T)
+    if not flag_dev:
+        raise RuntimeError("graph mode needs the any-live flags in mapped host memory")
+    gs = getattr(sim, "_graph_state", None)
+    if gs is None or gs["act"] is not act or gs["key"] != (is_eval, G, T):
+        gs = sim._graph_state = {
+            "act": act, "key": (is_eval, G, T), "graphs": [],
+            "obs": sim.empty_obs(), "success": torch.zeros(n, dtype=torch.int8, device=dev),
+            "seqs": torch.full((T, n), -1, dtype=torch.int32, device=dev),
+            "refs": None if is_eval else torch.empty((T + 1, n), dtype=torch.int32, device=dev),
+            "bc": None if is_eval else torch.zeros(n, dtype=torch.uint8, device=dev)}
+    obs, success, seqs, refs = gs["obs"], gs["success"], gs["seqs"], gs["refs"]
+    sim.reset(*spec, obs=obs)
+    success.zero_()
+    seqs.fill_(-1)
+    if not is_eval:
+        gs["bc"].copy_(_bc_mask(behavior_clone, n, dev))
+        sim.teacher(action_out=refs[0])          # the initial states' labels; then every step's
+    nch = (T + G - 1) // G
+    if not gs["graphs"]:
+        step = _stepper(sim, not is_eval, gs["bc"], success)
+
+        def issue(t):
+            actions = act(obs, t)
+            actions = actions.to(device=dev, dtype=torch.int32).reshape(n).contiguous()
+            step(t, actions, obs, None if is_eval else refs[t], seqs[t], flag_dev + 4 * t,
+                 None if is_eval else refs[t + 1])
+
+        main = torch.cuda.current_stream(dev)
+        warm = torch.cuda.Stream(dev)            # the student's libraries warmed off the capture
+        warm.wait_stream(main)
+        with torch.cuda.stream(warm):
+            act(obs, 0)
+        main.wait_stream(warm)
+        pool = None
+        for c in range(nch):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                for t in range(c * G, min(T, (c + 1) * G)):
+                    issue(t)
+            pool = g.pool()
+            gs["graphs"].append(g)
+    graphs = gs["graphs"]
+    t_loop = time.perf_counter()
+    graphs[0].replay()
+    events[0].record()
+    ticks = None
+    c = 0
+    while ticks is None:
+        if c + 1 < nch:                          # queued before chunk c's flags are read
+            graphs[c + 1].replay()
+            events[c + 1].record()
+        events[c].synchronize()
+        for t in range(c * G, min(T, (c + 1) * G)):
+            if int(flags[t]) == 0:               # every episode ended at tick t (imitation.py:42)
+                ticks = t + 1
+                break
+        c += 1
+        if ticks is None and c >= nch:
+            ticks = T
+    if not is_eval and receive is not None:
+        labels = refs[:ticks].clone()
+        for t in range(ticks):
+            receive(labels[t])
+    t_end_loop = time.perf_counter()
+    return _finish(sim, spec, task, success.clone(), seqs.clone(), ticks, is_eval, False, None,
+                   torch.arange(n, dtype=torch.int32, device=dev), timing, t_start, t_loop,
+                   t_end_loop, dev)
 
 
 def _live_flags(sim, T):

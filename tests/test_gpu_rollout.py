@@ -181,3 +181,50 @@ def test_host_flag_pointer(gpu):
     assert N.lib().craft_host_flag_pointer(pinned.data_ptr(), ctypes.byref(p)) == 0 and p.value
     plain = torch.zeros(8, dtype=torch.int32)
     assert N.lib().craft_host_flag_pointer(plain.data_ptr(), ctypes.byref(p)) == N.EINVAL
+
+
+@pytest.mark.parametrize("is_eval,bc_rate,stop_at,G", [(False, 0.5, None, 8), (False, 0.0, 6, 7),
+                                                       (True, 0.0, 9, 40), (False, 0.0, 17, 1)])
+def test_graph_rollout_equals_sync_loop(gpu, is_eval, bc_rate, stop_at, G):
+    """do_rollout(graph=G) (HIP graphs of G ticks, captured once per simulator and act, replayed
+    by later rollouts) gives the synchronous loop's result bit for bit at 65,536 envs: two
+    rollouts on different specs and cloning masks through the same graphs, early stops inside
+    and at the end of a chunk, every receive() call."""
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import do_rollout
+    from psketch_amd.sim import sample_scenarios, synthetic_specs
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 256)
+    n = 65536
+    rng = np.random.RandomState(4)
+    W = rng.randint(-3, 4, size=(4, cfg.n_features, 6))
+    bias = np.asarray([0, 1, 2, 3, 4, 0])
+    base = torch_policy(W, bias, gpu)
+
+    def act(obs, t):
+        a = base(obs, t)
+        return torch.full_like(a, 5) if stop_at is not None and t >= stop_at else a
+
+    ref_sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    ref_sim.load_pool(pool)
+    g_sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    g_sim.load_pool(pool)
+    for rep in range(2):
+        spec = synthetic_specs(pool, 12, 12, n, seed=3 + rep, task_ids=[t.id for t in tm.dataset_tasks()])
+        bc = rng.binomial(1, bc_rate, size=n)
+        outs = []
+        for sim, graph in ((ref_sim, 0), (g_sim, G)):
+            received = []
+            info = do_rollout(sim, spec, act, is_eval, behavior_clone=bc,
+                              receive=lambda r: received.append(r.cpu().numpy()), graph=graph)
+            outs.append((info, received))
+        (a, ra), (b, rb) = outs
+        assert a.ticks == b.ticks == (stop_at + 1 if stop_at is not None else cfg.max_timesteps)
+        for k in ("action_seqs", "n_actions", "success", "distances", "is_get"):
+            assert torch.equal(getattr(a, k), getattr(b, k)), (rep, k)
+        assert (a.num_interactions, a.num_steps) == (b.num_interactions, b.num_steps)
+        assert len(ra) == len(rb) == (0 if is_eval else a.ticks)
+        for x, y in zip(ra, rb):
+            assert np.array_equal(x, y)
+    assert len(g_sim._graph_state["graphs"]) == (cfg.max_timesteps + G - 1) // G
