@@ -79,10 +79,10 @@ def parse(argv=None):
                         "trainer: configs[2]/[4] closed loop, psketch_amd.rollout.do_rollout "
                         "(train mode, fused teacher labels, a fixed on-device student); "
                         "--steps counts rollouts")
-    p.add_argument("--rollout-graph", type=int, default=0,
+    p.add_argument("--rollout-graph", type=int, default=8,
                    help="trainer workload: ticks per captured HIP graph in do_rollout (0 = the "
-                        "eager lookahead loop; 8 measured the same, 78.9 against 76-79 us per "
-                        "tick: the loop is bound by the kernels and their dispatch gaps)")
+                        "eager lookahead loop: 2.9-3.2 ms per 40-tick rollout against 2.80-2.91 "
+                        "with graphs of 8 ticks, whose loop does not depend on the host's speed)")
     p.add_argument("--teacher-mode", choices=("fused", "separate"), default="fused",
                    help="teacher workload: one craft_step_teach launch per tick, or craft_teacher "
                         "then craft_step")

@@ -221,6 +221,11 @@ int craft_sim_set_obs_format(craft_sim_t* sim, int32_t format);
  * the last call (then clears it); *env_out receives the offending slot. */
 int craft_sim_check(craft_sim_t* sim, int64_t* env_out, void* stream);
 
+/* Without synchronising: queues a copy of the latched-error record into device int32[4]
+ * `out` on `stream` ({status, 0, slot low, slot high}; status 0 = no error), so a caller can
+ * read it back together with its own results and call craft_sim_check only when it is set. */
+int craft_sim_error_word(craft_sim_t* sim, int32_t* out, void* stream);
+
 /* ---- scenario pool ---------------------------------------------------------- */
 
 /* Uploads `count` initial grids (host, count * W*H kind ids, x-major) into pool

@@ -113,6 +113,7 @@ SIGNATURES = {
     "craft_sim_info": (_i32, [_vp, ctypes.POINTER(_i64), ctypes.POINTER(_i32),
                               ctypes.POINTER(_i32)]),
     "craft_sim_check": (_i32, [_vp, ctypes.POINTER(_i64), _vp]),
+    "craft_sim_error_word": (_i32, [_vp, _vp, _vp]),
     "craft_sim_tune": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),

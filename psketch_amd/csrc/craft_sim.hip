@@ -587,6 +587,13 @@ int craft_sim_check(craft_sim_t* s, int64_t* env_out, void* stream) {
   return CRAFT_OK;
 }
 
+int craft_sim_error_word(craft_sim_t* s, int32_t* out, void* stream) {
+  if (!s || !out) return CRAFT_EINVAL;
+  HIP_TRY(s, hipMemcpyAsync(out, s->d_err, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                            reinterpret_cast<hipStream_t>(stream)));
+  return CRAFT_OK;
+}
+
 int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t count) {
   if (!s || !grids || first < 0 || count < 0) return fail(s, CRAFT_EINVAL, "craft_pool_load: bad argument");
   if ((int64_t)first + count > s->pool_capacity) return fail(s, CRAFT_ERANGE, "craft_pool_load: beyond pool capacity");

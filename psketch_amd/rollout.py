@@ -333,8 +333,11 @@ def _live_flags(sim, T):
 
 def _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot_ids, timing,
             t_start, t_loop, t_end_loop, dev):
+    """The rollout's summary (imitation.py:79-99) with one read-back: the distances of failed
+    get tasks (their initial grid at the final pose, find_closest_resources' length), queued
+    whether or not there are any; then the episode counters, the None-success and unreachable-
+    target tests and the latched-error word come back together."""
     n = sim.n_envs
-    # distances (imitation.py:79-91): failed get tasks, initial grid at the final pose
     get_ids = getattr(sim, "_get_task_ids", None)
     if get_ids is None:
         get_ids = sim._get_task_ids = torch.as_tensor(
@@ -342,31 +345,28 @@ def _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot
             dtype=torch.int32, device=dev)
     is_get = torch.isin(task, get_ids)
     probe = is_get & (success == 0)
-    # one read-back for: stats since the reset (env-steps = envs live at the start
-    # of each tick = num_interactions, imitation.py:54; minus episodes ended =
-    # transitions = num_steps, :71), a None success, any distance to compute
+    st = sim.get_state(fields=("agent",))
+    sim.set_state(torch.stack(spec, dim=1), st["agent"])
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    sim.teacher(slots=torch.where(probe, slot_ids, -1), path_len_out=lens)
+    distances = torch.where(probe, lens, torch.where(is_get, 0, -1).to(torch.int32))
+    n_actions = (seqs >= 0).sum(dim=0).to(torch.int32)
+    # stats since the reset (env-steps = envs live at the start of each tick = num_interactions,
+    # imitation.py:54; minus episodes ended = transitions = num_steps, :71), a None success, an
+    # unreachable target, the error word
     summary = torch.cat([sim.stats(), (success < 0).any().reshape(1).to(torch.int64),
-                         probe.any().reshape(1).to(torch.int64)]).cpu().tolist()
-    _, ended, env_steps, bad_success, any_probe = summary
-    num_interactions = 0 if is_eval else env_steps
-    num_steps = 0 if is_eval else env_steps - ended
-    distances = torch.where(is_get, 0, -1).to(torch.int32)
-    lens = None
-    if any_probe:
-        st = sim.get_state(fields=("agent",))
-        sim.set_state(torch.stack(spec, dim=1), st["agent"])
-        lens = torch.empty(n, dtype=torch.int32, device=dev)
-        sim.teacher(slots=torch.where(probe, slot_ids, -1), path_len_out=lens)
-    sim.check()                                  # errors latched in the loop or the probe
+                         (probe & (lens < 0)).any().reshape(1).to(torch.int64),
+                         sim.error_word()[:1].to(torch.int64)]).cpu().tolist()
+    _, ended, env_steps, bad_success, unreachable, err = summary
+    if err:
+        sim.check()                              # raises: an error latched in the loop or the probe
     if bad_success:
         raise RolloutError("satisfies() returned None for a finished episode (imitation.py:68)")
-    if lens is not None:
-        if bool((probe & (lens < 0)).any()):
-            raise RolloutError("find_closest_resources found no target: len(None) (imitation.py:88-89)")
-        distances = torch.where(probe, lens, distances)
-    n_actions = (seqs >= 0).sum(dim=0).to(torch.int32)
+    if unreachable:
+        raise RolloutError("find_closest_resources found no target: len(None) (imitation.py:88-89)")
+    num_interactions = 0 if is_eval else env_steps
+    num_steps = 0 if is_eval else env_steps - ended
     if timing is not None:
-        torch.cuda.synchronize(dev)
         t_done = time.perf_counter()
         for k, v in (("setup", t_loop - t_start), ("loop", t_end_loop - t_loop),
                      ("summary", t_done - t_end_loop), ("ticks", t)):

@@ -155,6 +155,16 @@ class CraftSim:
         self._check(N.lib().craft_sim_check(self._h, ctypes.byref(slot), self._stream()),
                     "kernel error")
 
+    def error_word(self, out=None):
+        """Device int32[4] copy of the latched-error record ({status, 0, slot lo, slot hi}),
+        queued on the current stream without synchronising (craft_sim_error_word)."""
+        if out is None:
+            out = torch.empty(4, dtype=torch.int32, device=self.device)
+        self._buf("out", out, torch.int32, (4,))
+        self._check(N.lib().craft_sim_error_word(self._h, _ptr(out), self._stream()),
+                    "craft_sim_error_word")
+        return out
+
     # ---- helpers --------------------------------------------------------------------
     def _i32(self, x, n=None):
         if x is None:
