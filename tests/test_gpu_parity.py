@@ -298,11 +298,15 @@ def test_bad_action_latches_error():
     sim.reset(*synthetic_specs(pool, 12, 12, 64, 0, seed=0, task_ids=[12]))
     acts = torch.zeros(64, dtype=torch.int32, device="cuda")
     acts[17] = 9
+    assert sim.error_word().cpu().tolist() == [0, 0, 0, 0]
     sim.step(acts, tick=0)
+    w = sim.error_word().cpu().tolist()   # queued on the stream, read without craft_sim_check
+    assert w[0] == N.EBADACTION and w[2] == 17
     with pytest.raises(N.CraftError) as e:
         sim.check()
     assert e.value.status == N.EBADACTION
     sim.check()   # cleared
+    assert sim.error_word().cpu().tolist()[0] == 0
 
 
 def test_pool_rejects_open_border():
