@@ -87,3 +87,63 @@ def test_obs_format_argument():
     assert bench.parse(["--obs-format", "u8"]).obs_format == "u8"
     with pytest.raises(SystemExit):
         bench.parse(["--obs-format", "f16"])
+
+
+def test_pmc_traffic_lookup(tmp_path):
+    """roofline.traffic comes from the PMC entry of the same workload and ticks per launch."""
+    import json
+    f = tmp_path / "t.json"
+    f.write_text(json.dumps([
+        {"workload": "w", "ticks_per_launch": 20, "hbm_bytes_per_launch": 1.0},
+        {"workload": "w", "ticks_per_launch": 32, "hbm_bytes_per_launch": 2.0},
+        {"workload": "x", "ticks_per_launch": 1, "hbm_bytes_per_launch": 3.0}]))
+    a = types.SimpleNamespace(traffic=str(f))
+    assert bench.pmc_traffic(a, "w", 20) == 1.0
+    assert bench.pmc_traffic(a, "w", 32) == 2.0
+    assert bench.pmc_traffic(a, "x", 1) == 3.0
+    assert bench.pmc_traffic(a, "w", 1) is None
+    assert bench.pmc_traffic(types.SimpleNamespace(traffic=str(tmp_path / "none.json")), "w", 20) is None
+
+
+def test_pmc_summary_corrections(tmp_path, monkeypatch):
+    """tools/pmc_summary.py: FETCH_SIZE doubled (gfx950 counts half of wide reads), KiB ->
+    bytes, the dominant kernel by total duration, the first (warmup) launch left out of the
+    per-launch trace mean."""
+    import csv
+    import json
+    import sys
+    sys.path.insert(0, str(bench.REPO) + "/tools")
+    import pmc_summary
+    src = tmp_path / "src"
+    (src / "trace").mkdir(parents=True)
+    line = {"config": {"workload": "w"}, "roofline": {"ticks_per_launch": 20, "kernel_us": 10.0,
+                                                       "bytes_per_launch": 1000}}
+    (src / "bench.json").write_text(json.dumps(line) + "\n")
+    with open(src / "trace" / "run_kernel_stats.csv", "w", newline="") as fh:
+        w = csv.DictWriter(fh, ["Name", "Calls", "TotalDurationNs", "AverageNs"])
+        w.writeheader()
+        w.writerow({"Name": "k", "Calls": 3, "TotalDurationNs": 90, "AverageNs": 30})
+        w.writerow({"Name": "small", "Calls": 1, "TotalDurationNs": 5, "AverageNs": 5})
+    with open(src / "trace" / "run_kernel_trace.csv", "w", newline="") as fh:
+        w = csv.DictWriter(fh, ["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for s, e in ((0, 10000), (20000, 60000), (70000, 110000)):
+            w.writerow({"Kernel_Name": "k", "Start_Timestamp": s, "End_Timestamp": e})
+    for c, v in (("FETCH_SIZE", 2.0), ("WRITE_SIZE", 8.0)):
+        (src / f"pmc_{c}").mkdir()
+        with open(src / f"pmc_{c}" / "run_counter_collection.csv", "w", newline="") as fh:
+            w = csv.DictWriter(fh, ["Kernel_Name", "Counter_Value"])
+            w.writeheader()
+            w.writerow({"Kernel_Name": "k", "Counter_Value": v})
+            w.writerow({"Kernel_Name": "small", "Counter_Value": 100.0})
+    top = tmp_path / "profiles" / "pmc_traffic.json"
+    top.parent.mkdir()
+    top.write_text("[]")
+    monkeypatch.setattr(pmc_summary.os.path, "abspath", lambda p: str(tmp_path / "tools" / "x.py"))
+    pmc_summary.main(str(src), str(tmp_path / "dst"))
+    e = json.loads((tmp_path / "dst" / "pmc_traffic.json").read_text())[0]
+    assert e["kernel"] == "k" and e["ticks_per_launch"] == 20
+    assert e["hbm_read_bytes_per_launch"] == 2 * 2.0 * 1024
+    assert e["hbm_write_bytes_per_launch"] == 8.0 * 1024
+    assert e["rocprof_avg_us_after_first"] == 40.0
+    assert json.loads(top.read_text())[0]["workload"] == "w"

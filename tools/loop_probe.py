@@ -4,7 +4,9 @@ gaps between them count:
 
   policy   the stand-in student alone (addmm + argmax + int32 cast), 40 ticks
   step     craft_step_teach alone (student actions precomputed), 40 ticks
+  step_plain / teacher   craft_step_ex and craft_teacher alone
   both     policy then step per tick, 40 ticks (one do_rollout's device work)
+  side_teacher   craft_teacher on a side stream beside the policy, then craft_step_ex
   graph    `both` captured as one HIP graph and replayed
 
     python tools/loop_probe.py [--envs 65536] [--reps 5]
@@ -44,10 +46,30 @@ def main():
     def step(t, a):
         sim.step(a, tick=t, autoreset=True, obs=obs, labels=labels[t + 1])
 
+    side = torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    ev = [torch.cuda.Event() for _ in range(T)]
+
+    def step_plain(t, a):
+        sim.step(a, tick=t, autoreset=True, obs=obs)
+
+    def side_tick(t):
+        # the teacher's labels of the current states on a side stream, beside the student
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            sim.teacher(action_out=labels[t])
+        ev[t].record(side)
+        a = policy(t)
+        main.wait_event(ev[t])
+        step_plain(t, a)
+
     seqs = {
         "policy": lambda: [policy(t) for t in range(T)],
         "step": lambda: [step(t, acts) for t in range(T)],
+        "step_plain": lambda: [step_plain(t, acts) for t in range(T)],
+        "teacher": lambda: [sim.teacher(action_out=labels[t]) for t in range(T)],
         "both": lambda: [step(t, policy(t)) for t in range(T)],
+        "side_teacher": lambda: [side_tick(t) for t in range(T)],
     }
     sim.reset(*specs)
     for f in seqs.values():
