@@ -292,6 +292,10 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       if (ag && ((ti >> 8) & 1u)) {
         action = -1;                                                     // frozen: the label of a done env
       } else if (ag) {
+#ifdef CRAFT_ABL_NOTEACH
+        action = CRAFT_STOP;                                             // ablation build only
+      } else if (false) {
+#endif
         Agent s{};
         s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};

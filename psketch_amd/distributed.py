@@ -20,13 +20,14 @@ def world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def init(device=None, backend=None):
+def init(device=None, backend=None, force=False):
     """Initialise the process group when WORLD_SIZE > 1 (RCCL for GPUs, gloo on
     CPU; backend="gloo" with a GPU device keeps the data on the GPU and runs the
     two scalar collectives through host copies — a rehearsal of several ranks on
-    one card)."""
+    one card).  force=True initialises a one-rank group too (the RCCL path on a
+    one-GPU box)."""
     rank, ws, _ = world()
-    if ws > 1 and not dist.is_initialized():
+    if (ws > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if device is not None and device.type == "cuda" else "gloo"
         kw = {"device_id": device} if backend == "nccl" and device is not None else {}
@@ -50,8 +51,9 @@ def env_shard(rank, envs_per_rank):
     return rank * envs_per_rank, envs_per_rank
 
 
-def active():
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+def active(any_size=False):
+    """A process group with more than one rank (any_size: with at least one)."""
+    return dist.is_available() and dist.is_initialized() and (any_size or dist.get_world_size() > 1)
 
 
 def reduce_episode_stats(stats):

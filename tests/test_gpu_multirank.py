@@ -35,3 +35,39 @@ def test_two_ranks_on_one_card_equal_one_process():
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 8192
     assert two["episodes"] == one["episodes"]
     assert two["episodes"]["env_steps"] > 8192 * 25      # warmup + timed + the event-timed launches
+
+
+_RCCL_ONE_RANK = r"""
+import torch, torch.distributed as dist
+from psketch_amd import distributed as D
+dev = torch.device("cuda:0")
+D.init(device=dev, force=True)
+assert dist.get_backend() == "nccl", dist.get_backend()
+stats = torch.tensor([3, 7, 1 << 40], dtype=torch.int64, device=dev)
+D._reduce(stats, dist.ReduceOp.SUM)
+torch.cuda.synchronize()
+assert stats.tolist() == [3, 7, 1 << 40], stats.tolist()
+t = torch.tensor([2.5], dtype=torch.float64, device=dev)
+D._reduce(t, dist.ReduceOp.MAX)
+assert t.item() == 2.5
+D.barrier()
+dist.barrier()
+dist.destroy_process_group()
+print("rccl-ok")
+"""
+
+
+def test_rccl_process_group_on_the_card():
+    """The nccl (= RCCL) branch of distributed.init with device_id, and the int64[3] summary
+    and float64 max all-reduces bench.py issues, executed over RCCL on the GPU (one rank: a
+    one-GPU box cannot hold two RCCL ranks on one device)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    out = subprocess.run([sys.executable, "-c", _RCCL_ONE_RANK], cwd=REPO, env=env, capture_output=True,
+                         text=True, timeout=180)
+    assert out.returncode == 0 and "rccl-ok" in out.stdout, (out.stdout[-1000:], out.stderr[-2000:])

@@ -26,7 +26,7 @@ def main():
     p.add_argument("--teacher", action="store_true")
     p.add_argument("--obs-store", type=int, nargs="+", default=[1],
                    help="observation store policies to time (craft_sim_tune: 0 wb, 1 nt, 2 sc1)")
-    p.add_argument("--cfg", nargs="+", default=["0:0"],
+    p.add_argument("--cfg", nargs="*", default=["0:0"],
                    help="step kernel knobs EPW:PER_CU (craft_sim_tune_step; 0 = auto / no cap)")
     args = p.parse_args()
     n = args.envs
@@ -90,11 +90,6 @@ def main():
                 for k, name in ((2, "teach_tick2"), (1, "teach_tile")):
                     sim.tune_teach(k)
                     res[f"{name}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
-                sim.tune_teach(3)
-                for cfg in args.cfg:
-                    epw, per_cu = (int(x) for x in cfg.split(":"))
-                    sim.tune_step(2, epw, per_cu)
-                    res[f"teach_step_{cfg}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
             sim.tune(0, 0, 2)
             sim.tune_step(0)
             sim.tune_teach(0)
