@@ -356,6 +356,22 @@ int craft_transition(craft_sim_t* sim, const int32_t* src, const int32_t* dst,
 int craft_observe(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32_t* tasks,
                   void* obs, int8_t* sat, void* stream);
 
+/* The per-env part of the rollout's summary (trainers/imitation.py:79-91), one launch over
+ * every slot after a do_rollout: tasks int32[n] (each slot's task), success int8[n]
+ * (1 / 0 / -1 for None), action_seqs int32[ticks][n] (the action record, -1 where the env did
+ * not act).  Per slot: is_get_out = the task's goal is `get`; distances_out = -1 for other
+ * goals, 0 for a success, else len(find_closest_resources(task.arg)) on world.init_state(
+ * grid, pos, dir): the slot's initial grid (its pool row, nothing cleared) at its current pose
+ * (-2 where the reference raises, base.py:31; CRAFT_ETEACHER latches); n_actions_out = the
+ * action record's non-negative entries (len(action_seqs[i])).  flags_out int32[2] (zeroed
+ * here): [0] some success is None (imitation.py:68 asserts), [1] a failed get task has no
+ * reachable target (len(None), imitation.py:88-89).  The env states are not modified.
+ * Replaces trainers/imitation.py:79-91's per-env loop. */
+int craft_rollout_distances(craft_sim_t* sim, const int32_t* tasks, const int8_t* success,
+                            const int32_t* action_seqs, int32_t ticks, int32_t* distances_out,
+                            uint8_t* is_get_out, int32_t* n_actions_out, int32_t* flags_out,
+                            void* stream);
+
 /* DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for n slots:
  * find_incomplete_subtask over the hint tree then the BFS of
  * find_closest_resources/shortest_path (teachers/base.py:10-87).

@@ -136,6 +136,7 @@ SIGNATURES = {
     "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "craft_observe": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "craft_teacher": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
+    "craft_rollout_distances": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
     "craft_get_state": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "craft_set_state": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "craft_sample_scenarios": (_i32, [_i32, _i32, _i32, _vp, _i32, _i32, _vp, _i32, _u32,

@@ -16,6 +16,9 @@ hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const Tile
                        hipStream_t st);
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st);
+hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, const int8_t* success,
+                            const int32_t* seqs, int32_t ticks, int64_t n, int32_t* dist_out,
+                            uint8_t* is_get_out, int32_t* n_actions_out, int32_t* flags, hipStream_t st);
 hipError_t launch_rollout(int win, int tile, int threads, const SimView& v, const RolloutArgs& a, size_t lds,
                           hipStream_t st);
 hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t st);
@@ -882,6 +885,24 @@ int craft_observe(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
   a.obs = obs;
   a.sat = sat;
   return launch(s, craft::MODE_OBSERVE, a, stream, "craft_observe launch");
+}
+
+int craft_rollout_distances(craft_sim_t* s, const int32_t* tasks, const int8_t* success,
+                            const int32_t* action_seqs, int32_t ticks, int32_t* distances_out,
+                            uint8_t* is_get_out, int32_t* n_actions_out, int32_t* flags_out, void* stream) {
+  if (!s) return CRAFT_EINVAL;
+  if (!tasks || !success || !distances_out || !is_get_out || !n_actions_out || !flags_out || ticks < 0 ||
+      (ticks > 0 && !action_seqs))
+    return fail(s, CRAFT_EINVAL, "craft_rollout_distances: bad argument");
+  if (4 * s->view.C > 1000)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_distances: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  HIP_TRY(s, hipMemsetAsync(flags_out, 0, 2 * sizeof(int32_t), st));
+  if (s->n_envs == 0) return CRAFT_OK;
+  hipError_t e = craft::launch_distances((s->view.C + 31) / 32, s->view, tasks, success, action_seqs, ticks,
+                                         s->n_envs, distances_out, is_get_out, n_actions_out, flags_out, st);
+  if (e != hipSuccess) return hip_fail(s, e, "craft_rollout_distances launch");
+  return CRAFT_OK;
 }
 
 int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t* tasks, int32_t* action_out,

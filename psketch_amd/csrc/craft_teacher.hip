@@ -95,6 +95,103 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   }
 }
 
+// ---- the rollout's per-env summary (craft_rollout_distances) ----------------------------------
+struct DistArgs {
+  const int32_t* tasks;
+  const int8_t* success;
+  const int32_t* seqs;       // [ticks][n] action record, -1 where the env did not act
+  int32_t ticks;
+  int64_t n;
+  int32_t* dist_out;
+  uint8_t* is_get_out;
+  int32_t* n_actions_out;
+  int32_t* flags;            // [2]: a None success, an unreachable target (plain stores of 1)
+};
+
+// trainers/imitation.py:79-91 for env i, LANES lanes per env: is_get = task i's goal is `get`;
+// distances[i] = -1 for other goals, 0 for a success, else len(find_closest_resources(task.arg))
+// on world.init_state(grid_i, pos, dir): the env's initial grid (its pool row: no cleared cells)
+// at the final pose.  Only that BFS runs, as the reference calls only find_closest_resources.
+// n_actions[i] counts the action record (len(action_seqs[i])).
+template <int NW, int LANES>
+__global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
+  __shared__ uint16_t s_tab[CRAFT_MAX_TASKS];
+  for (int t = threadIdx.x; t < v.n_tasks; t += blockDim.x) s_tab[t] = v.task_tab[t];
+  __syncthreads();
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
+  const int ql = (int)(threadIdx.x % LANES);
+  if (i >= a.n) return;                  // lane-group-uniform
+  const bool lead = ql == 0;
+  const int task = a.tasks[i];
+  const int succ = a.success[i];
+  if (task < 0 || task >= v.n_tasks) {
+    if (lead) {
+      latch_error(v.err, CRAFT_ERANGE, i);
+      a.dist_out[i] = -2;
+      a.is_get_out[i] = 0;
+      a.n_actions_out[i] = 0;
+    }
+    return;
+  }
+  const uint32_t tt = s_tab[task];
+  const bool is_get = (tt & 0xf) == CRAFT_GOAL_GET;
+  int d = is_get ? 0 : -1;
+  if (is_get && succ == 0 && ((tt >> 4) & 0xffu) == 0) {
+    d = -1;                              // kind 0 is never a target (as teach_env)
+  } else if (is_get && succ == 0) {
+    const Agent s = unpack_state(v.state[i]);
+    if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
+      if (lead) latch_error(v.err, CRAFT_EINVAL, i);
+      d = -2;
+    } else {
+      const int C = v.C, nq = (C + 3) >> 2;
+      Bits<NW> valid = bzero<NW>();
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int nb = min(32, max(0, C - w * 32));
+        valid.w[w] = nb >= 32 ? ~0u : ((1u << nb) - 1u);
+      }
+      const uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
+      Bits<NW> occ, tgt;
+      grid_bits<NW, LANES>(row32, nq, m, (tt >> 4) & 0xffu, ql, valid, occ, tgt);
+      int fa = -1, len = -1;
+      const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, v.H, s.x * v.H + s.y, s.dir, ql, fa, len, false,
+                                             v.pool_conn[s.scen] != 0);
+      d = ok ? len : -2;                 // -2: the reference raises (base.py:31 len(None))
+      if (lead && !ok) latch_error(v.err, CRAFT_ETEACHER, i);
+    }
+  }
+  if (lead) {
+    int na = 0;
+    for (int t = 0; t < a.ticks; ++t) na += a.seqs[(int64_t)t * a.n + i] >= 0;
+    a.dist_out[i] = d;
+    a.is_get_out[i] = is_get;
+    a.n_actions_out[i] = na;
+    if (succ < 0) a.flags[0] = 1;
+    if (d == -1 && is_get && succ == 0) a.flags[1] = 1;
+  }
+}
+
+hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, const int8_t* success,
+                            const int32_t* seqs, int32_t ticks, int64_t n, int32_t* dist_out,
+                            uint8_t* is_get_out, int32_t* n_actions_out, int32_t* flags, hipStream_t st) {
+  DistArgs a{tasks, success, seqs, ticks, n, dist_out, is_get_out, n_actions_out, flags};
+  const int lanes = n <= kTeacherQuadMaxItems ? 4 : 2;
+  const unsigned blocks = (unsigned)((lanes * n + 255) / 256);
+#define CRAFT_DIST(NWV)                                                                                 \
+  do {                                                                                                  \
+    if (lanes == 4) hipLaunchKernelGGL((distances_kernel<NWV, 4>), dim3(blocks), dim3(256), 0, st, v, a); \
+    else hipLaunchKernelGGL((distances_kernel<NWV, 2>), dim3(blocks), dim3(256), 0, st, v, a);          \
+  } while (0)
+  if (nw <= 2) CRAFT_DIST(2);
+  else if (nw <= 4) CRAFT_DIST(4);
+  else if (nw <= 5) CRAFT_DIST(5);
+  else CRAFT_DIST(8);
+#undef CRAFT_DIST
+  return hipGetLastError();
+}
+
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
   TeachArgs a{slots, tasks, n, act_out, len_out};

@@ -14,9 +14,11 @@ a kernel on the current stream:
 The student sees the features as a device tensor and returns device actions;
 nothing crosses PCIe inside the loop except the all(done) test (imitation.py:42):
 the step kernels store each tick's any-live flag straight into page-locked host
-memory, which the host reads once the tick's event has completed.  After the loop, `distances` (imitation.py:79-91) come
-from the same teacher kernel: failed get-tasks are reset to their initial grid
-at their final position and find_closest_resources' length is read back.
+memory, which the host reads once the tick's event has completed.  After the loop, one
+launch (craft_rollout_distances) computes every env's `distances` entry (imitation.py:79-91:
+failed get tasks search their initial grid from their final pose with
+find_closest_resources' BFS), is_get and action count, and the summary comes back in one
+transfer.
 """
 import ctypes
 import time
@@ -27,7 +29,6 @@ import torch
 from . import _native as N
 from .sim import CraftSim
 
-GOAL_GET = "get"
 
 
 class RolloutError(Exception):
@@ -106,7 +107,6 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
         raise ValueError("max_timesteps must be positive")
     spec = [sim._i32(a, n) for a in spec]
     task = spec[4]
-    slot_ids = torch.arange(n, dtype=torch.int32, device=dev)
     obs_hist = (torch.empty((T + 1, n, sim.n_features), dtype=sim.obs_dtype, device=dev)
                 if keep_obs else None)
     obs = obs_hist[0] if keep_obs else sim.empty_obs()
@@ -191,8 +191,8 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
     if side is not None:
         main.wait_stream(side)
     t_end_loop = time.perf_counter()
-    return _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot_ids,
-                   timing, t_start, t_loop, t_end_loop, dev)
+    return _finish(sim, task, success, seqs, t, is_eval, keep_obs, obs_hist, timing, t_start,
+                   t_loop, t_end_loop, dev)
 
 
 def _stepper(sim, teach, bc, success):
@@ -310,9 +310,8 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
         for t in range(ticks):
             receive(labels[t])
     t_end_loop = time.perf_counter()
-    return _finish(sim, spec, task, success.clone(), seqs.clone(), ticks, is_eval, False, None,
-                   torch.arange(n, dtype=torch.int32, device=dev), timing, t_start, t_loop,
-                   t_end_loop, dev)
+    return _finish(sim, task, success.clone(), seqs.clone(), ticks, is_eval, False, None, timing,
+                   t_start, t_loop, t_end_loop, dev)
 
 
 def _live_flags(sim, T):
@@ -331,39 +330,39 @@ def _live_flags(sim, T):
     return flags, sim._live_dev, sim._live_events
 
 
-def _finish(sim, spec, task, success, seqs, t, is_eval, keep_obs, obs_hist, slot_ids, timing,
-            t_start, t_loop, t_end_loop, dev):
-    """The rollout's summary (imitation.py:79-99) with one read-back: the distances of failed
-    get tasks (their initial grid at the final pose, find_closest_resources' length), queued
-    whether or not there are any; then the episode counters, the None-success and unreachable-
-    target tests and the latched-error word come back together."""
+def _finish(sim, task, success, seqs, t, is_eval, keep_obs, obs_hist, timing, t_start, t_loop,
+            t_end_loop, dev):
+    """The rollout's summary (imitation.py:79-99) with one read-back: one launch computes every
+    env's distance (failed get tasks: find_closest_resources' length on the initial grid at the
+    final pose), is_get and action count (craft_rollout_distances); then the episode counters,
+    the None-success and unreachable-target flags and the latched-error word come back in one
+    transfer."""
     n = sim.n_envs
-    get_ids = getattr(sim, "_get_task_ids", None)
-    if get_ids is None:
-        get_ids = sim._get_task_ids = torch.as_tensor(
-            [i for i, tk in enumerate(sim.task_manager.tasks) if tk.goal_name == GOAL_GET],
-            dtype=torch.int32, device=dev)
-    is_get = torch.isin(task, get_ids)
-    probe = is_get & (success == 0)
-    st = sim.get_state(fields=("agent",))
-    sim.set_state(torch.stack(spec, dim=1), st["agent"])
-    lens = torch.empty(n, dtype=torch.int32, device=dev)
-    sim.teacher(slots=torch.where(probe, slot_ids, -1), path_len_out=lens)
-    distances = torch.where(probe, lens, torch.where(is_get, 0, -1).to(torch.int32))
-    n_actions = (seqs >= 0).sum(dim=0).to(torch.int32)
-    # stats since the reset (env-steps = envs live at the start of each tick = num_interactions,
-    # imitation.py:54; minus episodes ended = transitions = num_steps, :71), a None success, an
-    # unreachable target, the error word
-    summary = torch.cat([sim.stats(), (success < 0).any().reshape(1).to(torch.int64),
-                         (probe & (lens < 0)).any().reshape(1).to(torch.int64),
-                         sim.error_word()[:1].to(torch.int64)]).cpu().tolist()
-    _, ended, env_steps, bad_success, unreachable, err = summary
+    task = task.contiguous()
+    buf = getattr(sim, "_summary_buf", None)
+    if buf is None:   # int64 [0:3] stats, [3] the two flags (int32), [4:6] the error word (int32[4])
+        buf = sim._summary_buf = torch.zeros(6, dtype=torch.int64, device=dev)
+    distances = torch.empty(n, dtype=torch.int32, device=dev)
+    is_get = torch.empty(n, dtype=torch.uint8, device=dev)
+    n_actions = torch.empty(n, dtype=torch.int32, device=dev)
+    sim._check(N.lib().craft_rollout_distances(
+        sim._h, task.data_ptr(), success.data_ptr(), seqs.data_ptr(), seqs.shape[0],
+        distances.data_ptr(), is_get.data_ptr(), n_actions.data_ptr(), buf[3:4].data_ptr(),
+        torch._C._cuda_getCurrentRawStream(dev.index)), "craft_rollout_distances")
+    sim.stats(out=buf[0:3])
+    sim.error_word(out=buf[4:6].view(torch.int32))
+    summary = buf.cpu()
+    flags = summary[3:4].view(torch.int32).tolist()
+    _, ended, env_steps = summary[:3].tolist()
+    bad_success, unreachable = flags
+    err = int(summary[4:6].view(torch.int32)[0])
     if err:
         sim.check()                              # raises: an error latched in the loop or the probe
     if bad_success:
         raise RolloutError("satisfies() returned None for a finished episode (imitation.py:68)")
     if unreachable:
         raise RolloutError("find_closest_resources found no target: len(None) (imitation.py:88-89)")
+    is_get = is_get.view(torch.bool)
     num_interactions = 0 if is_eval else env_steps
     num_steps = 0 if is_eval else env_steps - ended
     if timing is not None:
