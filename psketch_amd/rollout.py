@@ -348,7 +348,7 @@ def _finish(sim, task, success, seqs, t, is_eval, keep_obs, obs_hist, timing, t_
     sim._check(N.lib().craft_rollout_distances(
         sim._h, task.data_ptr(), success.data_ptr(), seqs.data_ptr(), seqs.shape[0],
         distances.data_ptr(), is_get.data_ptr(), n_actions.data_ptr(), buf[3:4].data_ptr(),
-        torch._C._cuda_getCurrentRawStream(dev.index)), "craft_rollout_distances")
+        sim._stream()), "craft_rollout_distances")
     sim.stats(out=buf[0:3])
     sim.error_word(out=buf[4:6].view(torch.int32))
     summary = buf.cpu()

@@ -228,3 +228,50 @@ def test_graph_rollout_equals_sync_loop(gpu, is_eval, bc_rate, stop_at, G):
         for x, y in zip(ra, rb):
             assert np.array_equal(x, y)
     assert len(g_sim._graph_state["graphs"]) == (cfg.max_timesteps + G - 1) // G
+
+
+def test_rollout_distances_two_lane_path_vs_oracle(golden, gpu, oracle_mod):
+    """craft_rollout_distances above 8192 envs (2 BFS lanes per env): after a 16,384-env
+    eval rollout, a 384-env sample's distances equal the oracle's find_closest_resources length
+    on the env's initial grid at its final pose (imitation.py:83-89), its is_get the task's goal
+    and its action count the action record's; the env states are left as the rollout ended."""
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import do_rollout
+    from psketch_amd.sim import synthetic_specs
+    sc = golden("scenarios_seed123.npz")
+    pool = sc["w12_grids"]
+    world = "craft_medium_12x12"
+    _, _, tm, cfg = make_tables(world)
+    n = 16384
+    tasks = [t.id for t in tm.dataset_tasks()]
+    spec = np.stack(synthetic_specs(pool, 12, 12, n, seed=8, task_ids=tasks), axis=1)
+    spec[:, 3] = np.arange(n) % 4
+    rng = np.random.RandomState(4)
+    W = rng.randint(-3, 4, size=(3, cfg.n_features, 6))
+    bias = np.asarray([0, 1, 2, 3, 4, -40])
+    sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    sim.load_pool(pool)
+    info = do_rollout(sim, tuple(spec.T), torch_policy(W, bias, gpu), True)
+    agent = sim.get_state(fields=("agent",))["agent"].cpu().numpy()
+    dist, succ = info.distances.cpu().numpy(), info.success.cpu().numpy()
+    is_get, nact = info.is_get.cpu().numpy(), info.n_actions.cpu().numpy()
+    seqs = info.action_seqs.cpu().numpy()
+    o = oracle_mod.Oracle(cfg, pool)
+    get_ids = {t.id for t in tm.tasks if t.goal_name == "get"}
+    ids = np.random.RandomState(1).choice(n, 384, replace=False)
+    probed = 0
+    for i in ids:
+        tk = int(spec[i, 4])
+        assert bool(is_get[i]) == (tk in get_ids), i
+        assert nact[i] == int((seqs[:, i] >= 0).sum()), i
+        if tk not in get_ids:
+            assert dist[i] == -1, i
+        elif succ[i]:
+            assert dist[i] == 0, i
+        else:
+            e = o.env(pool[spec[i, 0]], agent[i, 0], agent[i, 1], agent[i, 2])
+            rc, _, ln = o.closest_resource(e, cfg.task[tk].arg_kind)
+            assert rc == 0 and dist[i] == ln, (i, dist[i], ln)
+            probed += 1
+    assert probed > 20
+    sim.check()
