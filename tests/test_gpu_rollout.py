@@ -275,3 +275,34 @@ def test_rollout_distances_two_lane_path_vs_oracle(golden, gpu, oracle_mod):
             probed += 1
     assert probed > 20
     sim.check()
+
+
+@pytest.mark.parametrize("case", ["none_success", "no_target"])
+def test_do_rollout_raises_where_the_reference_raises(golden, gpu, case):
+    """trainers/imitation.py's two failures at the end of a rollout, through the summary's
+    flags: satisfies() is None for a finished episode (a `use` task: the assert at :68), and a
+    failed get task whose initial grid holds none of its target (find_closest_resources returns
+    None, len(None) at :88-89).  Every env stops at tick 0 (a STOP-only student)."""
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import RolloutError, do_rollout
+    sc = golden("scenarios_seed123.npz")
+    pool = np.array(sc["w12_grids"][:4], dtype=np.uint8)
+    world = "craft_medium_12x12"
+    _, cb, tm, _ = make_tables(world)
+    task = {t.id: str(t) for t in tm.tasks}
+    if case == "none_success":
+        tid = next(i for i, s in task.items() if s == "use none")
+    else:
+        tid = next(i for i, s in task.items() if s == "get wood")
+        pool[0][pool[0] == cb.index["wood"]] = 0          # row 0 (the only one used) loses its wood
+    n = 300
+    free = [c for c in range(144) if pool[0][c] == 0 and 1 <= c // 12 <= 10 and 1 <= c % 12 <= 10]
+    cells = np.asarray(free)[np.arange(n) % len(free)]
+    spec = (np.zeros(n, np.int32), (cells // 12).astype(np.int32), (cells % 12).astype(np.int32),
+            np.zeros(n, np.int32), np.full(n, tid, np.int32))
+    sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    sim.load_pool(pool)
+    stop = torch.full((n,), 5, dtype=torch.int32, device=gpu)
+    with pytest.raises(RolloutError, match="None" if case == "none_success" else "len\\(None\\)"):
+        do_rollout(sim, spec, lambda obs, t: stop, True)
+    sim.check()                                           # nothing latched besides the flags
