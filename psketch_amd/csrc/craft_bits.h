@@ -80,6 +80,25 @@ __device__ __forceinline__ int bhighest(const Bits<NW>& a) {  // -1 if empty
     if (a.w[i]) r = i * 32 + 31 - __clz(a.w[i]);
   return r;
 }
+// The cells [lo, hi) as a set (0 <= lo <= hi <= 32 * NW).
+template <int NW>
+__device__ __forceinline__ Bits<NW> brange(int lo, int hi) {
+  Bits<NW> r;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int a = max(lo - 32 * i, 0), b = min(hi - 32 * i, 32);
+    r.w[i] = b <= a ? 0u : ((b - a >= 32 ? ~0u : ((1u << (b - a)) - 1u)) << a);
+  }
+  return r;
+}
+template <int NW>
+__device__ __forceinline__ int bcount(const Bits<NW>& a) {
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) c += __popc(a.w[i]);
+  return c;
+}
+
 // p -> p + d for every member (0 < |d| < 32); members shifted past either end drop out.
 template <int NW>
 __device__ __forceinline__ Bits<NW> bshift(const Bits<NW>& a, int d) {

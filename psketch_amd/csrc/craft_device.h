@@ -85,6 +85,10 @@ struct SimView {
 #define STAMP_END() do {} while (0)
 #endif
 
+// 32-bit words per cell set of the teacher's BFS (craft_teach.h: the band of grid columns
+// 1 .. W-2, the border columns left out); the kernels' NW template argument.
+__host__ __device__ inline int teach_words(int W, int H) { return ((W - 2) * H + 31) / 32; }
+
 struct LdsLayout {
   int obs, inv, task, rc, agent, ctrl, bytes;
 };

@@ -747,7 +747,7 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   a.label = label_out;
   int kernel = 0, envs = 0, tl = 0;
   step_shape(s, true, &kernel, &envs, &tl);
-  const int nw = (s->view.C + 31) / 32;
+  const int nw = craft::teach_words(s->view.W, s->view.H);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
   if (kernel == 2) {
@@ -899,7 +899,7 @@ int craft_rollout_distances(craft_sim_t* s, const int32_t* tasks, const int8_t* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(s, hipMemsetAsync(flags_out, 0, 2 * sizeof(int32_t), st));
   if (s->n_envs == 0) return CRAFT_OK;
-  hipError_t e = craft::launch_distances((s->view.C + 31) / 32, s->view, tasks, success, action_seqs, ticks,
+  hipError_t e = craft::launch_distances(craft::teach_words(s->view.W, s->view.H), s->view, tasks, success, action_seqs, ticks,
                                          s->n_envs, distances_out, is_get_out, n_actions_out, flags_out, st);
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout_distances launch");
   return CRAFT_OK;
@@ -914,7 +914,7 @@ int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
   if (4 * s->view.C > 1000)
     return fail(s, CRAFT_EINVAL, "craft_teacher: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
   if (n == 0) return CRAFT_OK;
-  hipError_t e = craft::launch_teacher((s->view.C + 31) / 32, s->view, slots, tasks, n, action_out,
+  hipError_t e = craft::launch_teacher(craft::teach_words(s->view.W, s->view.H), s->view, slots, tasks, n, action_out,
                                        path_len_out, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_teacher launch");
   return CRAFT_OK;

@@ -38,6 +38,22 @@ namespace craft {
 // cell ahead in their direction a is a target), so the level loop only tests
 // nxt_a & F_a; the faced targets themselves are formed on the rare levels that
 // have any.
+// The cell sets are kept over the band of columns 1 .. W-2 only (bit p = cell p + H of the
+// x-major grid): columns 0 and W-1 are the border, always occupied, never entered, so they are
+// left out (12x12: 120 bits = 4 words instead of 5).  What they contributed is that a LEFT move
+// from column 1 and a RIGHT move from column W-2 are blocked: these edge sets say so.  Rows 0
+// and H-1 stay in the band, so moves along a column need nothing.  Cell order is unchanged,
+// so `first in x-major order` comparisons are too.
+template <int NW>
+__device__ __forceinline__ Bits<NW> band_edge_lo(const Bits<NW>& valid, int H) {   // column 1
+  return brange<NW>(0, H);
+}
+template <int NW>
+__device__ __forceinline__ Bits<NW> band_edge_hi(const Bits<NW>& valid, int H) {   // column W-2
+  const int cb = bcount(valid);
+  return brange<NW>(cb - H, cb);
+}
+
 // One lane per query (LANES = 1): the same forward and backward passes, the four
 // actions of a level in one lane.
 template <int NW>
@@ -52,6 +68,8 @@ __device__ bool bfs_closest_1(const Bits<NW>& occ, const Bits<NW>& tgt, const Bi
     blk[a] = bshift(occ, -dl[a]);     // blk[a][p] = occ[p + dl[a]]
     fa[a] = bshift(tgt, -dl[a]);      // fa[a][p] = tgt[p + dl[a]]
   }
+  blk[2] = bor(blk[2], band_edge_lo<NW>(valid, H));   // the border columns left out of the band
+  blk[3] = bor(blk[3], band_edge_hi<NW>(valid, H));
   first_action = -1;
   path_len = -1;
   Bits<NW> claimed = bzero<NW>();
@@ -205,7 +223,11 @@ __device__ bool bfs_closest_2(const Bits<NW>& occ, const Bits<NW>& tgt, const Bi
   const uint32_t s = pl ? (uint32_t)H : 1u;     // lo action 2pl moves by -s, hi action 2pl + 1 by +s
   const int alo = 2 * pl;
   const Bits<NW> fr = bandn(valid, occ);
-  const Bits<NW> blk_lo = bshift_up(occ, s), blk_hi = bshift_dn(occ, s);   // blk[p] = occ[p + d]
+  Bits<NW> blk_lo = bshift_up(occ, s), blk_hi = bshift_dn(occ, s);         // blk[p] = occ[p + d]
+  if (pl) {                              // LEFT / RIGHT: the border columns left out of the band
+    blk_lo = bor(blk_lo, band_edge_lo<NW>(valid, H));
+    blk_hi = bor(blk_hi, band_edge_hi<NW>(valid, H));
+  }
   const Bits<NW> fa_lo = bshift_up(tgt, s), fa_hi = bshift_dn(tgt, s);     // fa[p] = tgt[p + d]
   const int dl0 = d0 == 0 ? -1 : d0 == 1 ? 1 : d0 == 2 ? -H : H;
   const uint32_t psh = __lane_id() & ~1u;                                  // this pair's lanes in a ballot
@@ -312,7 +334,9 @@ __device__ bool bfs_closest(const Bits<NW>& occ, const Bits<NW>& tgt, const Bits
     return bfs_closest_2<NW>(occ, tgt, valid, H, p0, d0, ql, first_action, path_len, want_action, conn);
   const int dla = ql == 0 ? -1 : ql == 1 ? 1 : ql == 2 ? -H : H;   // this lane's action
   const Bits<NW> fr = bandn(valid, occ);
-  const Bits<NW> blk = bshift_var(occ, -dla);                         // blk[p] = occ[p + dla]
+  Bits<NW> blk = bshift_var(occ, -dla);                               // blk[p] = occ[p + dla]
+  if (ql == 2) blk = bor(blk, band_edge_lo<NW>(valid, H));            // the border columns left
+  if (ql == 3) blk = bor(blk, band_edge_hi<NW>(valid, H));            // out of the band
   const Bits<NW> fa = bshift_var(tgt, -dla);                          // fa[p] = tgt[p + dla]
   const int dl0 = d0 == 0 ? -1 : d0 == 1 ? 1 : d0 == 2 ? -H : H;
   const uint32_t qsh = __lane_id() & ~3u;                             // this quad's lanes in a ballot
@@ -461,6 +485,25 @@ __device__ __forceinline__ void grid_bits(const uint32_t* row32, int nq, const u
   }
 }
 
+// grid_bits over the whole grid (C cells), then the band of columns 1 .. W-2 (bits H ..
+// C-H-1 moved down by H): NW band words from at most NW + 1 grid words.
+template <int NW, int LANES>
+__device__ __forceinline__ void band_bits(const uint32_t* row32, int nq, int C, int H, const uint32_t (&m)[8],
+                                          uint32_t kind, int ql, Bits<NW>& occ, Bits<NW>& tgt) {
+  constexpr int NF = NW + 1 < 8 ? NW + 1 : 8;
+  Bits<NF> of, tf;
+  grid_bits<NF, LANES>(row32, nq, m, kind, ql, brange<NF>(0, C), of, tf);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t o1 = i + 1 < NF ? of.w[i + 1] : 0u, t1 = i + 1 < NF ? tf.w[i + 1] : 0u;
+    occ.w[i] = __builtin_amdgcn_alignbit(o1, of.w[i], (uint32_t)H);
+    tgt.w[i] = __builtin_amdgcn_alignbit(t1, tf.w[i], (uint32_t)H);
+  }
+  const Bits<NW> vb = brange<NW>(0, C - 2 * H);
+  occ = band(occ, vb);
+  tgt = band(tgt, vb);
+}
+
 // DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for one env, LANES
 // lanes of a quad-aligned group (lane ql of the group).  Its current grid is row32
 // (kind ids, x-major, as 32-bit words; NW*8 words at most) minus the cells set in m
@@ -491,22 +534,17 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
     return -1;
   };
 
-  Bits<NW> valid = bzero<NW>();
-#pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    const int nb = min(32, max(0, C - w * 32));
-    valid.w[w] = nb >= 32 ? ~0u : ((1u << nb) - 1u);
-  }
+  const Bits<NW> valid = brange<NW>(0, C - 2 * H);      // the band of columns 1 .. W-2
   const int nq = (C + 3) >> 2;
   auto closest = [&](int kind, int& fa, int& len, bool want_action) -> bool {
     Bits<NW> occ, tgt;
-    grid_bits<NW, LANES>(row32, nq, m, (uint32_t)kind, ql, valid, occ, tgt);
+    band_bits<NW, LANES>(row32, nq, C, H, m, (uint32_t)kind, ql, occ, tgt);
 #ifdef CRAFT_ABL_NOBFS
     fa = (int)(occ.w[0] ^ tgt.w[NW - 1]) & 3;             // ablation build only: no BFS
     len = 1;
     return true;
 #endif
-    return bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y, s.dir, ql, fa, len, want_action, conn);
+    return bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y - H, s.dir, ql, fa, len, want_action, conn);
   };
   int leaf_kind = -1, leaf_fa = -1, leaf_len = -1;
   bool leaf_ok = true;

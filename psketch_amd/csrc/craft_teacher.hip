@@ -145,19 +145,14 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
       d = -2;
     } else {
       const int C = v.C, nq = (C + 3) >> 2;
-      Bits<NW> valid = bzero<NW>();
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const int nb = min(32, max(0, C - w * 32));
-        valid.w[w] = nb >= 32 ? ~0u : ((1u << nb) - 1u);
-      }
+      const Bits<NW> valid = brange<NW>(0, C - 2 * v.H);    // the band of columns 1 .. W-2
       const uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
       Bits<NW> occ, tgt;
-      grid_bits<NW, LANES>(row32, nq, m, (tt >> 4) & 0xffu, ql, valid, occ, tgt);
+      band_bits<NW, LANES>(row32, nq, C, v.H, m, (tt >> 4) & 0xffu, ql, occ, tgt);
       int fa = -1, len = -1;
-      const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, v.H, s.x * v.H + s.y, s.dir, ql, fa, len, false,
-                                             v.pool_conn[s.scen] != 0);
+      const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, v.H, s.x * v.H + s.y - v.H, s.dir, ql, fa, len,
+                                             false, v.pool_conn[s.scen] != 0);
       d = ok ? len : -2;                 // -2: the reference raises (base.py:31 len(None))
       if (lead && !ok) latch_error(v.err, CRAFT_ETEACHER, i);
     }
@@ -195,7 +190,8 @@ hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, cons
 hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
   TeachArgs a{slots, tasks, n, act_out, len_out};
-  // nw = 32-bit words per cell set: 8x8 -> 2, 10x10 -> 4, 12x12 -> 5, 16x16 -> 8
+  // nw = 32-bit words per BFS cell set (craft_teach.h: the band of columns 1 .. W-2):
+  // 8x8 -> 2, 10x10 -> 3 (run as 4), 12x12 -> 4, 16x16 -> 7 (run as 8)
   static const int forced = [] {                  // CRAFT_TEACHER_LANES=1/2/4: diagnostic override
     const char* e = getenv("CRAFT_TEACHER_LANES");
     const int x = e ? atoi(e) : 0;

@@ -37,7 +37,8 @@ static hipError_t launch_tt_win(int win, const SimView& v, const TileArgs& a, si
 
 template <int TL>
 static hipError_t launch_tt_nw(int nw, int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
-  // nw = 32-bit words per cell set: 8x8 -> 2, 10x10 -> 4, 12x12 -> 5, 16x16 -> 8
+  // nw = 32-bit words per BFS cell set (craft_teach.h: the band of columns 1 .. W-2):
+  // 8x8 -> 2, 10x10 -> 3 (run as 4), 12x12 -> 4, 16x16 -> 7 (run as 8)
   if (nw <= 2) return launch_tt_win<TL, 2>(win, v, a, lds, st);
   if (nw <= 4) return launch_tt_win<TL, 4>(win, v, a, lds, st);
   if (nw <= 5) return launch_tt_win<TL, 5>(win, v, a, lds, st);
