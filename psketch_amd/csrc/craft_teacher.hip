@@ -8,10 +8,10 @@
 
 namespace craft {
 
-// Batches up to this many items run 4 lanes per item, larger ones 2 (tools/ab_teach_lanes.sh,
-// profiles/r02/teach_lanes: 4096 items 12.1 / 15.9 / 25.5 us with 4 / 2 / 1 lanes, 32768
-// items 16.2 / 15.0 / 22.9, 65536 items 21.7 / 19.8 / 24.4).
-constexpr int64_t kTeacherQuadMaxItems = 8192;
+// Batches up to this many items run 4 lanes per item, larger ones 2 (profiles/r03/teacher_band,
+// the band-layout BFS: 4096 items 11.4 / 14.6 / 23.0 us with 4 / 2 / 1 lanes, 16384 items
+// 12.0 / 13.7 / 21.9, 65536 items 19.8 / 17.9 / 22.6; round 2, 32768 items: 16.2 / 15.0 / 22.9).
+constexpr int64_t kTeacherQuadMaxItems = 16384;
 
 struct TeachArgs {
   const int32_t* slots;

@@ -231,7 +231,7 @@ def test_graph_rollout_equals_sync_loop(gpu, is_eval, bc_rate, stop_at, G):
 
 
 def test_rollout_distances_two_lane_path_vs_oracle(golden, gpu, oracle_mod):
-    """craft_rollout_distances above 8192 envs (2 BFS lanes per env): after a 16,384-env
+    """craft_rollout_distances above 16,384 envs (2 BFS lanes per env): after a 32,768-env
     eval rollout, a 384-env sample's distances equal the oracle's find_closest_resources length
     on the env's initial grid at its final pose (imitation.py:83-89), its is_get the task's goal
     and its action count the action record's; the env states are left as the rollout ended."""
@@ -242,7 +242,7 @@ def test_rollout_distances_two_lane_path_vs_oracle(golden, gpu, oracle_mod):
     pool = sc["w12_grids"]
     world = "craft_medium_12x12"
     _, _, tm, cfg = make_tables(world)
-    n = 16384
+    n = 32768
     tasks = [t.id for t in tm.dataset_tasks()]
     spec = np.stack(synthetic_specs(pool, 12, 12, n, seed=8, task_ids=tasks), axis=1)
     spec[:, 3] = np.arange(n) % 4
