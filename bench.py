@@ -297,17 +297,29 @@ def profiled_kernel_us(fn, m, name):
 
 
 
-def run(args):
+def _init_ranks(args):
+    """torch.distributed.run's environment -> (rank, world_size, local_rank, device), with the
+    process group (RCCL when WORLD_SIZE > 1) initialised; the world size reported is the process
+    group's own (dist.get_world_size), which must agree with the launcher's."""
     import torch
-    from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
     from psketch_amd import distributed as D
-
     rank, world_size, local_rank = D.world()
     if args.one_device:
         local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    D.init(device=dev, backend=args.dist_backend)   # RCCL process group when WORLD_SIZE > 1
+    D.init(device=dev, backend=args.dist_backend)
+    if D.group_size() != world_size:
+        raise RuntimeError(f"process group has {D.group_size()} ranks, WORLD_SIZE={world_size}")
+    return rank, D.group_size(), local_rank, dev
+
+
+def run(args):
+    import torch
+    from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
+    from psketch_amd import distributed as D
+
+    rank, world_size, local_rank, dev = _init_ranks(args)
 
     teacher = args.workload == "teacher"
     K = 1 if teacher else args.ticks_per_launch
@@ -384,6 +396,7 @@ def run(args):
     t1 = time.perf_counter()
     D.barrier()
     elapsed = D.max_over_ranks(t1 - t0, dev)
+    local_s = t1 - t0
 
     # ---- per-launch kernel duration, HIP events on the launch stream (outside the timed
     # region): m back-to-back launches of k_eff ticks (as many as the timed region had, at
@@ -403,14 +416,16 @@ def run(args):
     prof_us = None
     if K == 1 and not args.no_kernel_profiler:
         if teacher and args.teacher_mode == "fused":
-            pname = {"tile_kernel": "tile_kernel", "tick2_kernel": "tick2_kernel",
-                     "step_kernel": "step_kernel"}[sim.step_shape(teach=True)[0]]
+            pname = sim.step_shape(teach=True)[0]
         else:
             pname = sim.step_shape()[0]
         prof_us = profiled_kernel_us(lambda: launch(1), min(m, 64), pname)
 
-    # ---- scalar episode summary: one RCCL all-reduce of int64[3] ----------------------------
-    stats = D.reduce_episode_stats(sim.stats()).cpu().tolist()
+    # ---- scalar episode summary: one RCCL all-reduce of int64[3]; every rank's own summary,
+    # shard and clock gathered over the process group for the line ---------------------------
+    local = sim.stats()
+    report = D.run_report(local_s, env_base, n, local.cpu().tolist(), dev)
+    stats = D.reduce_episode_stats(local).cpu().tolist()
     sim.check()
 
     if rank == 0:
@@ -431,7 +446,7 @@ def run(args):
         else:
             # what the library launches (craft_sim_step_shape), not a mirror of its defaults
             kn, kenvs, lanes = sim.step_shape(teach=teacher and args.teacher_mode == "fused")
-            kname = f"{kn}<{win}> ({kenvs} envs per {'wave' if kn == 'step_kernel' else 'workgroup'}"
+            kname = f"{kn}<{win}> ({kenvs} envs per workgroup"
             kname += f", {lanes} teacher lanes per env) (craft_step_teach)" if lanes else ") (craft_step)"
             if teacher and args.teacher_mode != "fused":
                 kname += " + teacher_kernel"
@@ -490,6 +505,7 @@ def run(args):
                                     f"({ceiling_slot_us:.1f} us per {ring[0].numel() * ring.element_size() / 1e6:.0f} MB "
                                     "slot), measured in this run before the timed region"},
             "episodes": {"successes": stats[0], "episodes": stats[1], "env_steps": stats[2]},
+            "dist": report,
         }
         if world_size == 1 and not args.no_cpu_baseline:
             c_leg = cpu_baseline_c(sim.config, grids, specs, env_base, args.seed, args.cpu_seconds,
@@ -521,27 +537,35 @@ def trainer_policy(n_features, device, seed=7, L=4):
     return act, W, bias
 
 
-def cpu_baseline_trainer(cfg, grids, specs, W, bias, bc, seconds):
+def cpu_baseline_trainer(cfg, grids, specs, W, bias, bc, seconds, n=256, max_rollouts=64):
     """oracle/rollout_oracle.py's do_rollout (trainers/imitation.py:18-101 one env at a time,
     with the C oracle's step / features / DemonstrationTeacher) and the same fixed policy in
-    numpy, on rollouts of 256 envs of the same workload, one core."""
+    numpy, on rollouts of n envs of the same workload, one core.  value = live env-steps/s:
+    num_interactions (imitation.py:54, one per env that has not finished, per tick: the env-ticks
+    the reference steps or ends), as the GPU line counts; slot_env_steps_per_s counts every env
+    slot every tick (n x the rollout's ticks = n x its student.receive calls)."""
     import oracle
     from oracle import rollout_oracle
     oracle.build()
     o = oracle.Oracle(cfg, grids)
     spec = np.stack(specs, axis=1)
     pol = rollout_oracle.fake_policy(W, bias)
-    n, steps, rollouts = 256, 0, 0
+    live = slots = ticks = rollouts = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds and rollouts < 64:
+    while time.perf_counter() - t0 < seconds and rollouts < max_rollouts:
         lo = (rollouts * n) % len(spec)
         sub = spec[lo:lo + n]
         info = rollout_oracle.do_rollout(o, sub, pol, False, bc_mask=bc[lo:lo + n])
-        steps += n * max(len(r) for r in info["received"]) if info["received"] else 0
+        live += info["num_interactions"]
+        ticks += len(info["received"])                  # one receive() per tick (imitation.py:77)
+        slots += len(sub) * len(info["received"])
         rollouts += 1
     dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{rollouts} rollouts of {n} envs ({steps} env-ticks, {dt:.1f} s): "
+    return {"value": live / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "slot_env_steps_per_s": slots / dt, "live_env_steps": live, "slot_env_ticks": slots,
+            "ticks": ticks, "rollouts": rollouts,
+            "sample": f"{rollouts} rollouts of {n} envs ({ticks} ticks, {live} live env-steps = "
+                      f"num_interactions, {slots} env-slot ticks, {dt:.1f} s): "
                       "oracle/rollout_oracle.py do_rollout (train mode, the C oracle's "
                       "DemonstrationTeacher every live env every tick, behaviour cloning) with "
                       "the same fixed policy in numpy, one core"}
@@ -553,18 +577,16 @@ def run_trainer(args):
     mode: every tick the student's act() on the device observations, then one
     craft_step_teach launch (behaviour cloning, the action record, the all(done) flag and the
     DemonstrationTeacher's labels for the next tick), the flag read one tick behind
-    (lookahead).  Value = env slots x ticks / s over every rank."""
+    (lookahead).  Value = live env-steps / s over every rank: num_interactions
+    (imitation.py:54), the env-ticks of envs that have not finished, which are what the reference
+    steps (a done env is skipped, imitation.py:63-73); slot_env_steps_per_s also counts the frozen
+    slots the batched loop carries until every episode has ended."""
     import torch
     from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
     from psketch_amd import distributed as D
     from psketch_amd.rollout import do_rollout
 
-    rank, world_size, local_rank = D.world()
-    if args.one_device:
-        local_rank = 0
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    D.init(device=dev, backend=args.dist_backend)
+    rank, world_size, local_rank, dev = _init_ranks(args)
     env_base, n = D.env_shard(rank, args.envs)
     sim = CraftSim(args.world, n_envs=n, device=local_rank, env_id_base=env_base,
                    pool_capacity=args.pool)
@@ -607,8 +629,10 @@ def run_trainer(args):
     t1 = time.perf_counter()
     D.barrier()
     elapsed = D.max_over_ranks(t1 - t0, dev)
-    tot = D.reduce_episode_stats(torch.as_tensor([n * ticks, live, ticks], dtype=torch.int64,
-                                                 device=dev)).cpu().tolist()
+    local = [n * ticks, live, ticks]
+    report = D.run_report(t1 - t0, env_base, n, local, dev,
+                          names=("slot_env_ticks", "live_env_steps", "ticks"))
+    tot = D.reduce_episode_stats(torch.as_tensor(local, dtype=torch.int64, device=dev)).cpu().tolist()
 
     # ---- per-tick split, outside the timed region: HIP events at the start and the end of the
     # student's kernels of every tick of one more rollout; the env launch (craft_step_teach)
@@ -647,7 +671,7 @@ def run_trainer(args):
         bps = bytes_per_env_step(sim.width, sim.height, win, F, True, 4)
         achieved = bps * n / (kernel_us * 1e-6) / 1e9
         workload = f"{args.world}_w{win}_B{n}_trainer_closed_loop_train_fused_teacher"
-        value = tot[0] / elapsed
+        value = tot[1] / elapsed                     # live env-steps (num_interactions)
         line = {
             "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
             "value": value,
@@ -667,11 +691,13 @@ def run_trainer(args):
                        "world": args.world, "envs_per_gpu": n, "global_batch": n * world_size,
                        "window": win, "n_features": F, "max_timesteps": sim.config.max_timesteps,
                        "rollouts": args.steps, "ticks": tot[2], "step": "one do_rollout "
-                       "(ticks until every episode has ended, <= max_timesteps); value counts every "
-                       "env slot every tick", "lookahead": True,
+                       "(ticks until every episode has ended, <= max_timesteps); value counts live "
+                       "env-steps (num_interactions, imitation.py:54: envs not yet done), "
+                       "slot_env_steps_per_s every env slot every tick", "lookahead": True,
                        "rollout_graph_ticks": args.rollout_graph,
                        "parallelism": f"env-shard x{world_size}"},
-            "live_env_steps_per_s": tot[1] / elapsed,
+            "slot_env_steps_per_s": tot[0] / elapsed,
+            "dist": report,
             "per_tick_us": {"timed_wall": elapsed * 1e6 / max(1, tot[2] // world_size),
                             "eager_wall": wall * 1e6, "policy": pol_us, "env": env_us,
                             "env_kernel_device": kernel_us,

@@ -173,21 +173,11 @@ int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t thread
  * reference (a tuning knob, like craft_sim_tune). */
 int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel);
 
-/* Which kernel craft_step / craft_step_ex launch: 0 (default) = the measured best (the tile
- * kernel), 1 = the tile kernel (craft_tile.h), 2 = the step kernel (craft_step.h: one
- * workgroup per CU, tick waves that load, step and scatter beside stream waves that store).  envs_per_wave: the
- * step kernel's envs per tick wave (16, 32, 64; 0 = by batch size), per_cu: at most that many
- * step workgroups per CU (pads the LDS request; 0 = no cap).  Results are identical for
- * every setting.  Replaces nothing in
- * the reference (a tuning knob). */
-int craft_sim_tune_step(craft_sim_t* sim, int32_t kernel, int32_t envs_per_wave, int32_t per_cu);
-
 /* The kernel craft_step / craft_step_ex (teach == 0) or craft_step_teach (teach != 0) will
- * launch, resolved from the knobs above: *kernel = CRAFT_KERNEL_STEP / _TILE / _TICK2, *envs =
- * envs per tick wave (step kernel), per tile (tile kernel) or per workgroup (two-tile kernel),
+ * launch, resolved from the knobs above: *kernel = CRAFT_KERNEL_TILE / _TICK2, *envs =
+ * envs per tile (tile kernel) or per workgroup (two-tile kernel),
  * *lanes = teacher lanes per env (0 without a teacher).  Lets a caller (bench.py) name the
  * kernel it times instead of mirroring the library's defaults. */
-#define CRAFT_KERNEL_STEP 0
 #define CRAFT_KERNEL_TILE 1
 #define CRAFT_KERNEL_TICK2 2
 int craft_sim_step_shape(const craft_sim_t* sim, int32_t teach, int32_t* kernel, int32_t* envs,
@@ -230,9 +220,11 @@ int craft_sim_error_word(craft_sim_t* sim, int32_t* out, void* stream);
 
 /* Uploads `count` initial grids (host, count * W*H kind ids, x-major) into pool
  * entries [first, first+count).  Replaces the `grid` handed to
- * CraftWorld.init_state (craft.py:258-259).  Rejects kind ids >= n_kinds and
- * worlds whose border ring is not fully occupied (every make_data.py world has
- * the boundary ring, make_data.py:108-112). Synchronous. */
+ * CraftWorld.init_state (craft.py:258-259).  Rejects (CRAFT_EINVARIANT) kind ids
+ * >= n_kinds and worlds whose border ring holds a cell that is empty, not inert
+ * (CRAFT_KIND_INERT: USE could clear it) or some task's target kind: every
+ * make_data.py world has the boundary ring (make_data.py:108-112), and the
+ * teacher's BFS and the kernels rely on it. Synchronous. */
 int craft_pool_load(craft_sim_t* sim, const uint8_t* grids, int32_t first, int32_t count);
 
 /* ---- episodes ---------------------------------------------------------------- */
@@ -325,7 +317,9 @@ int craft_step_teach(craft_sim_t* sim, const craft_step_args_t* args, int32_t* l
  * streams the caller orders): the work-unit counter they share is advanced by each launch, not
  * re-zeroed.  A launch captured into a HIP graph (hipStreamIsCapturing) uses a separate counter
  * that a memset captured with it zeroes, so a graph may be replayed any number of times, in
- * order with each other and with eager launches. */
+ * order with each other and with eager launches.  Every captured launch of one handle shares
+ * that one counter: two captured graphs, or one graph replayed on two streams, must never run
+ * concurrently (unsupported: their work units would be skipped or repeated, undetected). */
 int craft_rollout(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed, int64_t tick0,
                   int32_t n_ticks, uint32_t flags, void* obs, int32_t ring, float* reward,
                   uint8_t* done, int8_t* success, void* stream);
@@ -362,10 +356,11 @@ int craft_observe(craft_sim_t* sim, const int32_t* slots, int64_t n, const int32
  * not act).  Per slot: is_get_out = the task's goal is `get`; distances_out = -1 for other
  * goals, 0 for a success, else len(find_closest_resources(task.arg)) on world.init_state(
  * grid, pos, dir): the slot's initial grid (its pool row, nothing cleared) at its current pose
- * (-2 where the reference raises, base.py:31; CRAFT_ETEACHER latches); n_actions_out = the
- * action record's non-negative entries (len(action_seqs[i])).  flags_out int32[2] (zeroed
+ * (-1 where the grid holds no target, -2 where a target is unreachable: base.py:31); n_actions_out
+ * = the action record's non-negative entries (len(action_seqs[i])).  flags_out int32[2] (zeroed
  * here): [0] some success is None (imitation.py:68 asserts), [1] a failed get task has no
- * reachable target (len(None), imitation.py:88-89).  The env states are not modified.
+ * reachable target, in either case (the reference raises one TypeError, len(None), at
+ * imitation.py:88-89 or base.py:31).  The env states are not modified.
  * Replaces trainers/imitation.py:79-91's per-env loop. */
 int craft_rollout_distances(craft_sim_t* sim, const int32_t* tasks, const int8_t* success,
                             const int32_t* action_seqs, int32_t ticks, int32_t* distances_out,

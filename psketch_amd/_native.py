@@ -32,8 +32,8 @@ GOAL_OTHER, GOAL_GET, GOAL_MAKE, GOAL_GO, GOAL_USE = range(5)
 
 STEP_AUTORESET = 1
 
-KERNEL_STEP, KERNEL_TILE, KERNEL_TICK2 = 0, 1, 2
-KERNEL_NAMES = {KERNEL_STEP: "step_kernel", KERNEL_TILE: "tile_kernel", KERNEL_TICK2: "tick2_kernel"}
+KERNEL_TILE, KERNEL_TICK2 = 1, 2
+KERNEL_NAMES = {KERNEL_TILE: "tile_kernel", KERNEL_TICK2: "tick2_kernel"}
 
 
 class craft_recipe_t(ctypes.Structure):
@@ -118,7 +118,6 @@ SIGNATURES = {
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),
     "craft_sim_tune_teach": (_i32, [_vp, _i32]),
-    "craft_sim_tune_step": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_step_shape": (_i32, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                     ctypes.POINTER(_i32)]),
     "craft_sim_rollout_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32),

@@ -26,7 +26,6 @@ hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const Ti
                              hipStream_t st);
 hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
 size_t tick2_lds_bytes(int tl, int GS, int F);
-hipError_t launch_step(int win, int epw, size_t lds_min, const SimView& v, const TileArgs& a, hipStream_t st);
 
 namespace {
 
@@ -158,9 +157,6 @@ struct craft_sim {
   int rollout_obs_policy = 2;       // craft_rollout's observation stores until craft_sim_tune sets one:
                                     // write-through, 1.5 % faster than write-back (tools/ab_store.sh)
   int teach_kernel = 0;             // craft_sim_tune_teach: 0 auto, 1 one-tile, 2 two-tile
-  int step_kernel = 0;              // craft_sim_tune_step: 0 auto (the tile kernel), 1 tile, 2 step kernel
-  int step_epw_knob = 0;            // craft_sim_tune_step: envs per tick wave (0 auto)
-  int step_per_cu = 0;              // craft_sim_tune_step: step workgroups per CU cap (0 none)
   uint64_t queue1_next = 0;         // queue[1] (the split kernel's per-unit path) at the next launch
   uint64_t queue_next = 0;          // the counter's value at the next launch (every launch adds
                                     // its units + its grid: one fetch past the end per workgroup)
@@ -263,25 +259,13 @@ void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
   *split = (t <= 32 && nt >= 320) ? 1 : 0;
 }
 
-// Envs per tick wave of the step kernel (craft_step.h): 64 once that still gives one 4-wave
-// workgroup per CU (256 workgroups at 65,536 envs), else 32, else 16 (4096 envs: 64 workgroups).
-int step_epw(const craft_sim* s) {
-  if (s->step_epw_knob) return s->step_epw_knob;
-  if (s->n_envs >= 65536) return 64;
-  if (s->n_envs >= 32768) return 32;
-  return 16;
-}
-
 // What craft_step / craft_step_ex (teach = false) or craft_step_teach (teach = true) launches:
-// CRAFT_KERNEL_STEP (craft_step.h), CRAFT_KERNEL_TILE (craft_tile.h) or CRAFT_KERNEL_TICK2
-// (craft_tick2.h), with its envs per tick wave / tile and teacher lanes per env.
+// CRAFT_KERNEL_TILE (craft_tile.h) or CRAFT_KERNEL_TICK2 (craft_tick2.h), with its envs per
+// tile / workgroup and teacher lanes per env.
 void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lanes) {
   if (!teach) {
-    // auto: the tile kernel (the step kernel measured 28.2-29.6 us against 26.1-26.5
-    // at 65,536 envs with a 16-slot ring, 23.3 against 20.3 with one reused buffer)
-    const bool step = s->step_kernel == 2;
-    *kernel = step ? 0 : 1;
-    *envs = step ? step_epw(s) : s->tile;
+    *kernel = CRAFT_KERNEL_TILE;
+    *envs = s->tile;
     *lanes = 0;
     return;
   }
@@ -299,10 +283,6 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
   }();
   if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
   else { *kernel = 1; *envs = craft::kMaxTileEnvs; *lanes = tl1; }
-}
-
-size_t step_lds_min(const craft_sim* s) {
-  return s->step_per_cu > 0 ? (((size_t)163840 / s->step_per_cu) & ~size_t(15)) : 0;
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
@@ -483,20 +463,6 @@ int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel) {
   return CRAFT_OK;
 }
 
-int craft_sim_tune_step(craft_sim_t* s, int32_t kernel, int32_t envs_per_wave, int32_t per_cu) {
-  if (!s) return CRAFT_EINVAL;
-  if (kernel < 0 || kernel > 2)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: kernel must be 0 (auto), 1 (the tile kernel) or 2 (the step kernel)");
-  if (envs_per_wave != 0 && envs_per_wave != 16 && envs_per_wave != 32 && envs_per_wave != 64)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: envs_per_wave must be 0, 16, 32 or 64");
-  if (per_cu < 0 || per_cu > 16)
-    return fail(s, CRAFT_EINVAL, "craft_sim_tune_step: per_cu must be 0..16");
-  s->step_kernel = kernel;
-  s->step_epw_knob = envs_per_wave;
-  s->step_per_cu = per_cu;
-  return CRAFT_OK;
-}
-
 int craft_sim_step_shape(const craft_sim_t* s, int32_t teach, int32_t* kernel, int32_t* envs, int32_t* lanes) {
   if (!s) return CRAFT_EINVAL;
   int k = 0, e = 0, l = 0;
@@ -603,15 +569,27 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
   const int W = s->cfg.width, H = s->cfg.height, C = W * H, CS = s->view.CS;
   std::vector<uint8_t> staged((size_t)count * CS, 0);
   std::vector<uint8_t> conn((size_t)count, 0);
+  // Kinds a border cell may hold: occupied, inert under USE (never cleared, so the agent never
+  // reaches the border) and no task's target.  The teacher's band-layout BFS drops columns 0 and
+  // W-1 (craft_teach.h) and the kernels never index past the ring; make_data.py:108-112 and
+  // sample_scenario (craft.py:129-133) fill the ring with `boundary`, which qualifies.
+  uint32_t border_ok = 0;
+  for (int k = 1; k < s->cfg.n_kinds && k < 32; ++k)
+    if (s->cfg.kind_class[k] == CRAFT_KIND_INERT) border_ok |= 1u << k;
+  for (int t = 0; t < s->cfg.n_tasks; ++t)
+    if (s->cfg.task[t].arg_kind > 0 && s->cfg.task[t].arg_kind < 32) border_ok &= ~(1u << s->cfg.task[t].arg_kind);
   for (int p = 0; p < count; ++p) {
     const uint8_t* g = grids + (size_t)p * C;
     for (int c = 0; c < C; ++c) {
       if (g[c] >= s->cfg.n_kinds)
         return fail(s, CRAFT_EINVARIANT, "craft_pool_load: kind id out of range in grid " + std::to_string(first + p));
       const int x = c / H, y = c % H;
-      if ((x == 0 || y == 0 || x == W - 1 || y == H - 1) && g[c] == 0)
-        return fail(s, CRAFT_EINVARIANT, "craft_pool_load: grid " + std::to_string(first + p) +
-                                             " has an open border cell (make_data.py:108-112 builds a boundary ring)");
+      if ((x == 0 || y == 0 || x == W - 1 || y == H - 1) && !((border_ok >> g[c]) & 1u))
+        return fail(s, CRAFT_EINVARIANT, "craft_pool_load: grid " + std::to_string(first + p) + " border cell (" +
+                                             std::to_string(x) + ", " + std::to_string(y) + ") holds kind " +
+                                             std::to_string(g[c]) +
+                                             ": the ring must be occupied by inert, non-target kinds "
+                                             "(make_data.py:108-112 builds a boundary ring)");
     }
     std::memcpy(staged.data() + (size_t)p * CS, g, C);
     // are the free cells one 4-connected component?  Cells are only ever cleared next to the
@@ -767,12 +745,6 @@ int craft_step_ex(craft_sim_t* s, const craft_step_args_t* x, void* stream) {
   TileArgs a;
   const int rc = step_args(s, x, a);
   if (rc != CRAFT_OK) return rc;
-  if (s->step_kernel == 2) {
-    hipError_t e = craft::launch_step(s->cfg.window_width, step_epw(s), step_lds_min(s), s->view, a,
-                                      reinterpret_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(s, e, "craft_step launch");
-    return CRAFT_OK;
-  }
   return launch(s, craft::MODE_TICK, a, stream, "craft_step launch");
 }
 

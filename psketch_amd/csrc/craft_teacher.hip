@@ -153,8 +153,10 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
       int fa = -1, len = -1;
       const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, v.H, s.x * v.H + s.y - v.H, s.dir, ql, fa, len,
                                              false, v.pool_conn[s.scen] != 0);
-      d = ok ? len : -2;                 // -2: the reference raises (base.py:31 len(None))
-      if (lead && !ok) latch_error(v.err, CRAFT_ETEACHER, i);
+      // !ok: a target the BFS cannot reach.  The reference raises the same TypeError, len(None),
+      // whether no target exists or none (or a later one, base.py:31) is reachable, so both
+      // report through flags[1] below and nothing latches
+      d = ok ? len : -2;
     }
   }
   if (lead) {
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
     a.is_get_out[i] = is_get;
     a.n_actions_out[i] = na;
     if (succ < 0) a.flags[0] = 1;
-    if (d == -1 && is_get && succ == 0) a.flags[1] = 1;
+    if ((d == -1 || d == -2) && is_get && succ == 0) a.flags[1] = 1;
   }
 }
 

@@ -70,6 +70,49 @@ def max_over_ranks(value, device):
     return float(t.item())
 
 
+def _all_gather(t):
+    """all_gather of a small tensor; through host copies when the backend is gloo and t is on a
+    GPU.  Returns a list with one tensor per rank (on t's device)."""
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        out = [torch.empty_like(h) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, h)
+        return [o.to(t.device) for o in out]
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return out
+
+
+def group_size():
+    """World size as the process group reports it (1 without a process group)."""
+    return dist.get_world_size() if active(any_size=True) else 1
+
+
+def run_report(per_rank_s, env_id_base, n_envs, episodes, device,
+               names=("successes", "episodes", "env_steps")):
+    """What the process group itself says about the run, for the bench line: its backend and
+    world size (dist.get_backend / get_world_size, not the launcher's environment) and every
+    rank's timed seconds, shard (first global env id, env count) and local episode summary
+    {successes, episodes, env-steps}, all-gathered, so a line can be checked for shard
+    invariance against N = 1 on its own.  `episodes` holds one integer per name in `names`.
+    Without a process group: this process only."""
+    row = torch.tensor([dist.get_rank() if active(any_size=True) else 0, int(env_id_base), int(n_envs),
+                        *[int(x) for x in episodes], int(round(float(per_rank_s) * 1e9))],
+                       dtype=torch.int64, device=device)
+    if active(any_size=True):
+        rows, backend, ws = _all_gather(row), dist.get_backend(), dist.get_world_size()
+    else:
+        rows, backend, ws = [row], None, 1
+    ranks = []
+    for r in rows:
+        v = r.cpu().tolist()
+        k = len(names)
+        ranks.append({"rank": v[0], "env_id_base": v[1], "envs": v[2],
+                      "episodes": dict(zip(names, v[3:3 + k])), "per_rank_s": v[3 + k] * 1e-9})
+    return {"backend": backend, "world_size": ws, "process_group": backend is not None,
+            "per_rank_s": [r["per_rank_s"] for r in ranks], "ranks": ranks}
+
+
 def barrier():
     if active():
         dist.barrier()

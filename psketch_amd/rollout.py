@@ -21,7 +21,9 @@ find_closest_resources' BFS), is_get and action count, and the summary comes bac
 transfer.
 """
 import ctypes
+import inspect
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -243,15 +245,18 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
         raise ValueError("graph mode needs is_eval or fused_teacher")
     if G < 1:
         raise ValueError("graph: ticks per graph must be positive")
+    if T <= 0:
+        raise ValueError("max_timesteps must be positive")
     spec = [sim._i32(a, n) for a in spec]
     task = spec[4]
     flags, flag_dev, events = _live_flags(sim, T)
     if not flag_dev:
         raise RuntimeError("graph mode needs the any-live flags in mapped host memory")
     gs = getattr(sim, "_graph_state", None)
-    if gs is None or gs["act"] is not act or gs["key"] != (is_eval, G, T):
+    if gs is None or not _same_act(gs["act"], act) or gs["key"] != (is_eval, G, T):
+        sim._graph_state = None                  # drop the old graphs before capturing new ones
         gs = sim._graph_state = {
-            "act": act, "key": (is_eval, G, T), "graphs": [],
+            "act": _weak_act(act), "key": (is_eval, G, T), "graphs": [],
             "obs": sim.empty_obs(), "success": torch.zeros(n, dtype=torch.int8, device=dev),
             "seqs": torch.full((T, n), -1, dtype=torch.int32, device=dev),
             "refs": None if is_eval else torch.empty((T + 1, n), dtype=torch.int32, device=dev),
@@ -280,13 +285,19 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
             act(obs, 0)
         main.wait_stream(warm)
         pool = None
-        for c in range(nch):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                for t in range(c * G, min(T, (c + 1) * G)):
-                    issue(t)
-            pool = g.pool()
-            gs["graphs"].append(g)
+        graphs = []                              # cached only once every chunk is captured
+        try:
+            for c in range(nch):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    for t in range(c * G, min(T, (c + 1) * G)):
+                        issue(t)
+                pool = g.pool()
+                graphs.append(g)
+        except BaseException:
+            sim._graph_state = None              # a failed capture leaves nothing behind
+            raise
+        gs["graphs"] = graphs
     graphs = gs["graphs"]
     t_loop = time.perf_counter()
     graphs[0].replay()
@@ -312,6 +323,23 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
     t_end_loop = time.perf_counter()
     return _finish(sim, task, success.clone(), seqs.clone(), ticks, is_eval, False, None, timing,
                    t_start, t_loop, t_end_loop, dev)
+
+
+def _weak_act(act):
+    """A weak reference to the student's act for the graph cache, so the cache does not keep the
+    model alive (WeakMethod for a bound method: `student.act` is a new object on every access;
+    a plain strong reference for callables that take no weak references)."""
+    try:
+        return weakref.WeakMethod(act) if inspect.ismethod(act) else weakref.ref(act)
+    except TypeError:
+        return lambda: act
+
+
+def _same_act(ref, act):
+    """Whether the cached graphs were captured for this act: equality, which bound methods
+    define as the same function on the same object."""
+    cached = ref()
+    return cached is not None and cached == act
 
 
 def _live_flags(sim, T):

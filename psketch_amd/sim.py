@@ -97,16 +97,8 @@ class CraftSim:
         are identical for every setting."""
         self._check(N.lib().craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
 
-    def tune_step(self, kernel=0, envs_per_wave=0, per_cu=0):
-        """Which kernel step() launches without labels (craft_sim_tune_step): 0 the measured
-        best (the tile kernel), 1 the tile kernel, 2 the step kernel; the step kernel's envs
-        per tick wave (0 = by batch size) and workgroups-per-CU cap (0 = none); results are
-        identical for every setting."""
-        self._check(N.lib().craft_sim_tune_step(self._h, int(kernel), int(envs_per_wave), int(per_cu)),
-                    "craft_sim_tune_step")
-
     def step_shape(self, teach=False):
-        """(kernel name, envs per wave / tile / workgroup, teacher lanes per env) that step()
+        """(kernel name, envs per tile / workgroup, teacher lanes per env) that step()
         launches, without (teach=False) or with labels= (craft_sim_step_shape)."""
         k, e, l = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         self._check(N.lib().craft_sim_step_shape(self._h, int(bool(teach)), ctypes.byref(k),

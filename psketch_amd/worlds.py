@@ -100,9 +100,14 @@ class CraftWorld:
         self.random = getattr(config, "random", None)
 
         max_t = getattr(getattr(config, "trainer", None), "max_timesteps", gamedef.MAX_TIMESTEPS)
+        # the episode timer (trainers/imitation.py:29, timer = max_timesteps) is a u8 field of the
+        # packed state word (include/craft.h): refuse what it cannot hold instead of clamping
+        if int(max_t) != max_t or not 1 <= int(max_t) <= 255:
+            raise ValueError(f"CraftWorld: trainer.max_timesteps = {max_t!r}; the GPU episode timer "
+                             "holds 1 .. 255 ticks")
         self.sim = CraftSim(dict(self.params), n_envs=capacity, device=device,
                             pool_capacity=pool_capacity, recipes=recipes,
-                            hints=_hints_source(config), max_timesteps=min(int(max_t), 255))
+                            hints=_hints_source(config), max_timesteps=int(max_t))
         self.task_manager = self.sim.task_manager
         self._free = list(range(capacity - 1, -1, -1))
         self._pool = {}                  # grid bytes -> pool entry
@@ -111,7 +116,12 @@ class CraftWorld:
     # ---- slots ----------------------------------------------------------------------
     def _alloc(self):
         if not self._free:
-            raise RuntimeError("CraftWorld: all %d state slots are alive" % self.sim.n_envs)
+            # a slot comes back only when its CraftState is garbage-collected (CraftState.__del__)
+            raise RuntimeError(
+                f"CraftWorld: all {self.sim.n_envs} state slots are alive ({self.sim.n_envs} "
+                "CraftStates are still referenced; every step() keeps its predecessor alive "
+                "until the caller drops it). Drop old states or build the world with a larger "
+                f"capacity= (now {self.sim.n_envs})")
         return self._free.pop()
 
     def _release(self, slot):

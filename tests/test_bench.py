@@ -147,3 +147,42 @@ def test_pmc_summary_corrections(tmp_path, monkeypatch):
     assert e["hbm_write_bytes_per_launch"] == 8.0 * 1024
     assert e["rocprof_avg_us_after_first"] == 40.0
     assert json.loads(top.read_text())[0]["workload"] == "w"
+
+
+def test_trainer_cpu_leg_counts_live_env_steps():
+    """cpu_baseline_trainer counts live env-steps (num_interactions: one per env not yet done,
+    per tick, imitation.py:54) and env-slot ticks (envs x ticks), checked against
+    oracle/rollout_oracle.do_rollout run on the same rollouts (round 3 counted envs x envs)."""
+    import numpy as np
+    import oracle
+    from oracle import rollout_oracle
+    from psketch_amd.sim import sample_scenarios, synthetic_specs
+    from tests.helpers import make_tables
+    params, cb, tm, cfg = make_tables("craft_medium_12x12")
+    grids, _, _ = sample_scenarios(params, cb, 123, 16)
+    n, rollouts = 12, 3
+    specs = synthetic_specs(grids, 12, 12, n * rollouts, 0, seed=1,
+                            task_ids=[t.id for t in tm.dataset_tasks()])
+    rng = np.random.RandomState(2)
+    W = rng.randint(-3, 4, size=(4, cfg.n_features, 6))
+    bias = np.asarray([0, 1, 2, 3, 4, -8])
+    bc = rng.binomial(1, 0.5, size=n * rollouts)
+    leg = bench.cpu_baseline_trainer(cfg, grids, specs, W, bias, bc, seconds=600, n=n,
+                                     max_rollouts=rollouts)
+    oracle.build()
+    o = oracle.Oracle(cfg, grids)
+    spec = np.stack(specs, axis=1)
+    pol = rollout_oracle.fake_policy(W, bias)
+    live = ticks = 0
+    for r in range(rollouts):
+        info = rollout_oracle.do_rollout(o, spec[r * n:(r + 1) * n], pol, False,
+                                         bc_mask=bc[r * n:(r + 1) * n])
+        live += info["num_interactions"]
+        ticks += len(info["received"])
+        # a live env-step is an env acting before its episode ended: its action record
+        assert info["num_interactions"] == sum(len(a) for a in info["action_seqs"])
+    assert leg["rollouts"] == rollouts
+    assert leg["live_env_steps"] == live and leg["ticks"] == ticks
+    assert leg["slot_env_ticks"] == n * ticks
+    assert 0 < live <= n * ticks
+    assert leg["value"] == pytest.approx(leg["slot_env_steps_per_s"] * live / (n * ticks))

@@ -46,12 +46,26 @@ def _worker(rank, world_size, port, envs_per_rank, T, q):
     assert (r, ws) == (rank, world_size) and D.active()
     stats, obs_sum, specs = _run_shard(rank, envs_per_rank, T, pool, cfg)
     t = torch.tensor(stats, dtype=torch.int64)
+    report = D.run_report(0.5 * (rank + 1), D.env_shard(rank, envs_per_rank)[0], envs_per_rank,
+                          t.tolist(), torch.device("cpu"))
     D.reduce_episode_stats(t)
     mx = D.max_over_ranks(float(rank + 1), torch.device("cpu"))
     o = torch.tensor([obs_sum], dtype=torch.float64)
     torch.distributed.all_reduce(o)
-    q.put((rank, t.tolist(), mx, float(o.item()), [a.tolist() for a in specs]))
+    q.put((rank, t.tolist(), mx, float(o.item()), [a.tolist() for a in specs], report,
+           stats.tolist()))
     D.shutdown()
+
+
+def test_run_report_without_a_process_group():
+    """N = 1 without a process group: the line says so (backend None) and reports this process."""
+    from psketch_amd import distributed as D
+    rep = D.run_report(1.25, 0, 64, [1, 2, 3], torch.device("cpu"))
+    assert rep["backend"] is None and rep["world_size"] == 1 and rep["process_group"] is False
+    assert rep["ranks"] == [{"rank": 0, "env_id_base": 0, "envs": 64, "per_rank_s": 1.25,
+                             "episodes": {"successes": 1, "episodes": 2, "env_steps": 3}}]
+    rep = D.run_report(0.0, 8, 4, [5, 6, 7], torch.device("cpu"), names=("a", "b", "c"))
+    assert rep["ranks"][0]["episodes"] == {"a": 5, "b": 6, "c": 7}
 
 
 def test_two_rank_shards_equal_single_process():
@@ -70,10 +84,22 @@ def test_two_rank_shards_equal_single_process():
     from psketch_amd.sim import sample_scenarios, synthetic_specs
     pool, _, _ = sample_scenarios(params, cb, 123, 32)
     stats, obs_sum, specs = _run_shard(0, world_size * per, T, pool, cfg)
-    for rank, red, mx, osum, sp in res:
+    local = [r[6] for r in res]
+    for rank, red, mx, osum, sp, report, _ in res:
         assert red == stats.tolist()
         assert mx == float(world_size)
         assert osum == pytest.approx(obs_sum, rel=0, abs=0)
+        # the bench line's "dist" block: the process group's own backend and size, and every
+        # rank's shard, clock and local summary, identical on every rank
+        assert report["backend"] == "gloo" and report["world_size"] == world_size
+        assert report["process_group"] is True
+        assert [r["rank"] for r in report["ranks"]] == list(range(world_size))
+        assert [r["env_id_base"] for r in report["ranks"]] == [r * per for r in range(world_size)]
+        assert [r["envs"] for r in report["ranks"]] == [per] * world_size
+        assert report["per_rank_s"] == pytest.approx([0.5, 1.0])
+        assert [list(r["episodes"].values()) for r in report["ranks"]] == local
+        # shard invariance from the line alone: the per-rank summaries add up to N = 1's
+        assert np.sum(local, axis=0).tolist() == stats.tolist()
     cat = [np.concatenate([np.asarray(res[0][4][k]), np.asarray(res[1][4][k])]) for k in range(5)]
     for a, b in zip(cat, specs):
         np.testing.assert_array_equal(a, b)

@@ -35,6 +35,14 @@ def test_two_ranks_on_one_card_equal_one_process():
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 8192
     assert two["episodes"] == one["episodes"]
     assert two["episodes"]["env_steps"] > 8192 * 25      # warmup + timed + the event-timed launches
+    # the process group's own account (bench line "dist"), gathered over the group
+    d2, d1 = two["dist"], one["dist"]
+    assert d2["backend"] == "gloo" and d2["world_size"] == 2 and len(d2["per_rank_s"]) == 2
+    assert d1["backend"] is None and d1["world_size"] == 1
+    assert [r["env_id_base"] for r in d2["ranks"]] == [0, 4096]
+    assert sum(r["episodes"]["env_steps"] for r in d2["ranks"]) == one["episodes"]["env_steps"]
+    assert (sum(r["episodes"]["successes"] for r in d2["ranks"]) ==
+            d1["ranks"][0]["episodes"]["successes"])
 
 
 _RCCL_ONE_RANK = r"""

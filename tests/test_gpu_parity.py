@@ -309,11 +309,23 @@ def test_bad_action_latches_error():
     assert sim.error_word().cpu().tolist()[0] == 0
 
 
-def test_pool_rejects_open_border():
+@pytest.mark.parametrize("border", ["open", "wood", "water", "workshop0", "boundary"])
+def test_pool_border_ring(border):
+    """craft_pool_load refuses a border cell that is empty, clearable by USE (a grabbable kind,
+    water, stone) or a task's target (a workshop, wood), which the band-layout teacher BFS and
+    the kernels cannot see or would walk past; the boundary ring of every make_data.py world
+    (make_data.py:108-112) loads."""
     sim = CraftSim("craft_medium", n_envs=8, device=0, pool_capacity=2)
-    g = np.zeros((1, 64), dtype=np.uint8)
+    idx = sim.cookbook.index
+    g = np.zeros((8, 8), dtype=np.uint8)
+    g[0, :] = g[-1, :] = g[:, 0] = g[:, -1] = idx["boundary"]
+    if border != "boundary":
+        g[0, 3] = 0 if border == "open" else idx[border]
+    if border == "boundary":
+        sim.load_pool(g.reshape(1, 64))
+        return
     with pytest.raises(N.CraftError) as e:
-        sim.load_pool(g)
+        sim.load_pool(g.reshape(1, 64))
     assert e.value.status == N.EINVARIANT
 
 
@@ -508,14 +520,16 @@ def test_empty_and_single_env_calls(gpu):
     ((20, 3, 32), 16, -1),   # the continuous pipeline, incl. launches shorter than its prefetch
     ((32,), 32, 4),          # chunked units, ring >= launch: write-through state hand-off
     ((24,), 8, 3)])          # chunked units, ring < launch: full release between units
-def test_bench_rollout_equals_steps_at_full_size(launches, R, chunk):
+def test_bench_rollout_equals_steps_at_full_size(launches, R, chunk, oracle_mod):
     """BASELINE's single-GPU size (65536 envs, 12x12 craft_medium, w=3), the
     bench's own path: craft_rollout launches into a ring with the default
     workgroup shape, against one craft_step launch per tick.  Every
     observation, reward, done and success and the final states are identical
     (compared on the device), and the episode counters agree.  The chunked
     cases hand every tile between workgroups (possibly on other XCDs) several
-    times per launch, at full size."""
+    times per launch, at full size.  The rollout ring is also checked directly
+    against the CPU oracle: 256 random global ids, every tick the ring keeps, and
+    their agent states after each launch."""
     world = "craft_medium_12x12"
     params, cb, tm, cfg = make_tables(world)
     pool, _, _ = sample_scenarios(params, cb, 123, 1024)
@@ -531,19 +545,37 @@ def test_bench_rollout_equals_steps_at_full_size(launches, R, chunk):
             (("reward", torch.float32), ("done", torch.uint8), ("success", torch.int8))}
     obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
     one = {k: torch.empty(n, dtype=v.dtype, device="cuda") for k, v in outs.items()}
+    # the oracle on a sample of global ids, one env per call (its hashed actions are keyed by id)
+    gids = np.sort(np.random.RandomState(sum(launches) + R).choice(n, 256, replace=False))
+    o = oracle_mod.Oracle(cfg, pool)
+    envs = o.init_envs(*[np.asarray(s)[gids] for s in specs])
+    gid_d = torch.as_tensor(gids, device="cuda")
     t0 = 0
     for K in launches:
         a.rollout(K, seed=5, tick0=t0, obs=ring, **outs)
+        ref = []
         for t in range(t0, t0 + K):
             b.step(seed=5, tick=t, obs=obs, **one)
             if t >= t0 + K - R:                  # the ring keeps the launch's last R ticks
                 assert torch.equal(ring[t % R], obs), t
                 for k in outs:
                     assert torch.equal(outs[k][t % R], one[k]), (k, t)
+            step = [o.batch_tick(envs[j:j + 1], int(g), None, 5, t, True) for j, g in enumerate(gids)]
+            assert all(s[0] == 0 for s in step)
+            ref.append([np.concatenate([s[m] for s in step]) for m in range(1, 5)])
+        for t in range(max(t0, t0 + K - R), t0 + K):
+            r_obs, r_rew, r_done, r_succ = ref[t - t0]
+            np.testing.assert_array_equal(ring[t % R][gid_d].cpu().numpy(), r_obs, err_msg=f"obs {t}")
+            np.testing.assert_array_equal(outs["reward"][t % R][gid_d].cpu().numpy(), r_rew)
+            np.testing.assert_array_equal(outs["done"][t % R][gid_d].cpu().numpy(), r_done)
+            np.testing.assert_array_equal(outs["success"][t % R][gid_d].cpu().numpy(), r_succ)
         t0 += K
         sa, sb = a.get_state(), b.get_state()
         for k in sa:
             assert torch.equal(sa[k], sb[k]), k
+        np.testing.assert_array_equal(sa["agent"][gid_d].cpu().numpy(),
+                                      np.stack([envs["x"], envs["y"], envs["dir"], envs["timer"]], 1))
+        np.testing.assert_array_equal(sa["inventory"][gid_d].cpu().numpy(), envs["inv"][:, :cfg.n_kinds])
     np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
     assert host(a.stats())[2] == n * sum(launches)
     a.check()

@@ -277,12 +277,14 @@ def test_rollout_distances_two_lane_path_vs_oracle(golden, gpu, oracle_mod):
     sim.check()
 
 
-@pytest.mark.parametrize("case", ["none_success", "no_target"])
+@pytest.mark.parametrize("case", ["none_success", "no_target", "unreachable"])
 def test_do_rollout_raises_where_the_reference_raises(golden, gpu, case):
-    """trainers/imitation.py's two failures at the end of a rollout, through the summary's
+    """trainers/imitation.py's failures at the end of a rollout, through the summary's
     flags: satisfies() is None for a finished episode (a `use` task: the assert at :68), and a
-    failed get task whose initial grid holds none of its target (find_closest_resources returns
-    None, len(None) at :88-89).  Every env stops at tick 0 (a STOP-only student)."""
+    failed get task whose initial grid holds none of its target, or only a target walled in by
+    boundary cells (find_closest_resources returns None in both cases, and the reference raises
+    the same TypeError, len(None), at :88-89).  Every env stops at tick 0 (a STOP-only
+    student)."""
     from psketch_amd import CraftSim
     from psketch_amd.rollout import RolloutError, do_rollout
     sc = golden("scenarios_seed123.npz")
@@ -295,6 +297,11 @@ def test_do_rollout_raises_where_the_reference_raises(golden, gpu, case):
     else:
         tid = next(i for i, s in task.items() if s == "get wood")
         pool[0][pool[0] == cb.index["wood"]] = 0          # row 0 (the only one used) loses its wood
+        if case == "unreachable":                         # one wood, no free neighbour
+            g = pool[0].reshape(12, 12)
+            g[5, 5] = cb.index["wood"]
+            for x, y in ((4, 5), (6, 5), (5, 4), (5, 6)):
+                g[x, y] = cb.index["boundary"]
     n = 300
     free = [c for c in range(144) if pool[0][c] == 0 and 1 <= c // 12 <= 10 and 1 <= c % 12 <= 10]
     cells = np.asarray(free)[np.arange(n) % len(free)]

@@ -1,8 +1,6 @@
-"""The one-launch-per-tick kernels: the step kernel (csrc/craft_step.h, craft_sim_tune_step 2)
-identical to the tile kernel (craft_tile.h, the default) on every output of craft_step_ex
-across wave sizes, partial workgroups, windows and observation formats; and config 3's
-streamed tick (student actions, behaviour cloning, action record, any-live flag) at 65,536
-envs on the default kernel against the CPU oracle (trainers/imitation.py:43-73 per env)."""
+"""The one-launch-per-tick kernel (craft_tile.h): config 3's streamed tick (student actions,
+behaviour cloning, action record, any-live flag) at 65,536 envs against the CPU oracle
+(trainers/imitation.py:43-73 per env)."""
 import numpy as np
 import pytest
 import torch
@@ -22,51 +20,6 @@ def _outputs(sim, n, with_code=True):
             "action_record": torch.empty(n, dtype=torch.int32, device=dev),
             "any_live": torch.zeros(1, dtype=torch.int32, device=dev),
             "transition_code": torch.empty(n, dtype=torch.int8, device=dev) if with_code else None}
-
-
-# n picks the envs per tick wave (64 from 65,536, 32 from 32,768, else 16) and leaves a partial
-# last workgroup (and wave); windows 5 and 7 use 8- and 4-env scatter sub-chunks
-@pytest.mark.parametrize("world,W,n,T,fmt,autoreset", [
-    ("craft_medium_12x12", 12, 70001, 12, "f32", True),
-    ("craft_medium_12x12", 12, 40000, 25, "f32", False),
-    ("craft_medium_12x12", 12, 5000, 25, "bf16", True),
-    ("craft_medium_12x12", 12, 1000, 25, "u8", False),
-    ("craft_medium_12x12_w5", 12, 3001, 25, "f32", True),
-    ("craft_medium_12x12_w5", 12, 33000, 10, "u8", True),
-    ("craft_16x16_w7", 16, 1000, 25, "f32", True),
-    ("craft_16x16_w7", 16, 999, 20, "bf16", False),
-    ("craft_medium", 8, 2000, 25, "f32", True)])
-def test_step_kernel_equals_tile_kernel(world, W, n, T, fmt, autoreset):
-    params, cb, tm, cfg = make_tables(world)
-    pool, _, _ = sample_scenarios(params, cb, 123, 128)
-    specs = synthetic_specs(pool, W, W, n, 0, seed=3, task_ids=[t.id for t in tm.dataset_tasks()])
-    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
-    a.tune_step(2)
-    b.tune_step(1)
-    assert a.step_shape()[0] == "step_kernel" and b.step_shape()[0] == "tile_kernel"
-    assert a.step_shape()[1] == (64 if n >= 65536 else 32 if n >= 32768 else 16)
-    for s in (a, b):
-        s.set_obs_format(fmt)
-        s.reset(*specs)
-    oa, ob = _outputs(a, n), _outputs(b, n)
-    rng = np.random.RandomState(n)
-    for t in range(T):
-        acts = torch.as_tensor(rng.randint(0, 6, size=n).astype(np.int32), device="cuda")
-        ref = torch.as_tensor(rng.randint(0, 6, size=n).astype(np.int32), device="cuda")
-        bc = torch.as_tensor((rng.rand(n) < 0.3).astype(np.uint8), device="cuda")
-        hashed = t % 3 == 2                                       # the in-kernel draw on some ticks
-        for s, o in ((a, oa), (b, ob)):
-            o["any_live"].zero_()
-            s.step(None if hashed else acts, seed=7, tick=t, autoreset=autoreset,
-                   ref_actions=None if hashed else ref, behavior_clone=None if hashed else bc, **o)
-        for k in oa:
-            assert torch.equal(oa[k], ob[k]), f"{k} differs at tick {t}"
-    sa, sb = a.get_state(), b.get_state()
-    for k in sa:
-        assert torch.equal(sa[k], sb[k]), k
-    np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
-    a.check()
-    b.check()
 
 
 def test_step_ex_streamed_tick_full_size_vs_oracle(oracle_mod):

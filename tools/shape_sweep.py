@@ -42,8 +42,6 @@ def main():
                                           "32:320:0,32:384:0,32:512:0,64:256:0,64:512:0,32:512:-1,"
                                           "16:512:-1,0:0:0")
     ap.add_argument("--step", default="16:2,32:2,64:2,64:1,0:2")
-    ap.add_argument("--step-kernel", default="16:0,32:0,64:0",
-                    help="craft_step on the step kernel (craft_sim_tune_step 2): envs_per_wave:per_cu")
     args = ap.parse_args()
     n, R = args.envs, args.ring
     sim = CraftSim(args.world, n_envs=n, device=0, pool_capacity=1024)
@@ -97,17 +95,6 @@ def main():
             out[f"step_{spec}"] = {"shape": sim.tile_shape(), "us": round(us, 2),
                                    "gbs": round(bps * n / us / 1e3, 1)}
         sim.tune(0, 0, 2)
-        for spec in filter(None, args.step_kernel.split(",")):
-            epw, per_cu = (int(x) for x in spec.split(":"))
-            try:
-                sim.tune_step(2, epw, per_cu)
-                us = timed(step, args.reps * args.ticks)
-            except Exception as e:
-                out[f"stepk_{spec}"] = {"error": str(e)[:120]}
-                continue
-            out[f"stepk_{spec}"] = {"shape": sim.step_shape(), "us": round(us, 2),
-                                    "gbs": round(bps * n / us / 1e3, 1)}
-        sim.tune_step(0, 0, 0)
         sim.check()
         print(json.dumps(out), flush=True)
 

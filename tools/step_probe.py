@@ -26,8 +26,6 @@ def main():
     p.add_argument("--teacher", action="store_true")
     p.add_argument("--obs-store", type=int, nargs="+", default=[1],
                    help="observation store policies to time (craft_sim_tune: 0 wb, 1 nt, 2 sc1)")
-    p.add_argument("--cfg", nargs="*", default=["0:0"],
-                   help="step kernel knobs EPW:PER_CU (craft_sim_tune_step; 0 = auto / no cap)")
     args = p.parse_args()
     n = args.envs
     sim = CraftSim(args.world, n_envs=n, device=0, pool_capacity=1024)
@@ -72,18 +70,11 @@ def main():
                      labels=lab[r])
             st["t"] += 1
 
-        res = {"world": args.world, "envs": n, "ring": R, "fill_us": round(timeit(fill, args.iters), 2),
-               "stream_env": os.environ.get("CRAFT_STEP_STREAM", "")}
+        res = {"world": args.world, "envs": n, "ring": R, "fill_us": round(timeit(fill, args.iters), 2)}
         for pol in args.obs_store:
             sim.tune(0, 0, pol)
-            sim.tune_step(1)
             res[f"tile_p{pol}_us"] = round(timeit(step, args.iters), 2)
-            for cfg in args.cfg:
-                epw, per_cu = (int(x) for x in cfg.split(":"))
-                sim.tune_step(2, epw, per_cu)
-                res[f"step_{cfg}_p{pol}_us"] = round(timeit(step, args.iters), 2)
         sim.tune(0, 0, 2)
-        sim.tune_step(0)
         if args.teacher:
             for pol in args.obs_store:
                 sim.tune(0, 0, pol)
@@ -91,7 +82,6 @@ def main():
                     sim.tune_teach(k)
                     res[f"{name}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
             sim.tune(0, 0, 2)
-            sim.tune_step(0)
             sim.tune_teach(0)
         print(json.dumps(res), flush=True)
         del ring, rew, done, succ, lab
