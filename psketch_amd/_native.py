@@ -1,7 +1,9 @@
 """ctypes binding of the C ABI in include/craft.h (libpsketch_craft.so).
 
-The library is the product: every simulator call goes through it and there is
-no CPU fallback.  Importing this module without the built library raises.
+The HIP library is the product: every simulator call on a GPU goes through it and there is
+no CPU fallback; using it without the built library raises.  The CPU variant of the same ABI
+(libpsketch_craft_cpu.so, host pointers) is a separate library that only
+CraftSim(device="cpu") loads, on purpose.
 """
 import ctypes
 import os
@@ -12,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libpsketch_craft.so")
 # diagnostic builds (tools/) may point at another in-tree build of the same ABI
 LIB_PATH = os.environ.get("PSKETCH_CRAFT_LIB", LIB_PATH)
+CPU_LIB_PATH = os.path.join(_HERE, "lib", "libpsketch_craft_cpu.so")
 
 ABI_VERSION = 1
 MAX_KINDS = 32
@@ -149,35 +152,40 @@ class CraftError(RuntimeError):
         self.status = status
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """The loaded library; raises if it has not been built (no fallback)."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(cpu=False):
+    """The loaded HIP library (cpu=False) or the CPU variant of the same ABI (cpu=True); raises
+    if it has not been built (neither falls back to the other)."""
+    l = _libs.get(cpu)
+    if l is None:
+        path = CPU_LIB_PATH if cpu else LIB_PATH
+        if not os.path.exists(path):
             raise ImportError(
-                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
-                "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
-        l = ctypes.CDLL(LIB_PATH)
+                f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (hipcc --offload-arch=gfx950; g++ for the CPU variant). There is no "
+                "fallback.")
+        l = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = l
-    return _lib
+        _libs[cpu] = l
+    return l
 
 
-def strerror(status):
-    return lib().craft_strerror(status).decode()
+def strerror(status, L=None):
+    return (L or lib()).craft_strerror(status).decode()
 
 
-def check(status, handle=None, what=""):
+def check(status, handle=None, what="", L=None):
+    """Raise CraftError for a non-zero status; L: the library the handle belongs to."""
     if status != OK:
-        msg = strerror(status)
+        L = L or lib()
+        msg = strerror(status, L)
         if handle:
-            detail = lib().craft_sim_last_error(handle)
+            detail = L.craft_sim_last_error(handle)
             if detail:
                 msg = detail.decode()
         raise CraftError(status, f"{what}: {msg}" if what else msg)

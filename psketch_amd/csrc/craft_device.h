@@ -48,6 +48,7 @@ struct SimView {
   int32_t bridge, axe;
   int32_t obs_policy;         // observation stores: 0 write-back, 1 nontemporal, 2 write-through (sc1)
   int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
+  int32_t cpt;                // 1: the tile kernel stages compact records (craft_obs.h), 5x5 / 7x7 windows
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
   // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16.  Kernels copy the table to LDS.
@@ -80,9 +81,17 @@ struct SimView {
       v.stamps[8 * (int64_t)blockIdx.x + 7] = xcc;                                       \
     }                                                                                    \
   } while (0)
+// The latest time any wave reaches a point (lane 0 of each wave, a vector atomic max).
+#define STAMP_MAX(k)                                                                     \
+  do {                                                                                   \
+    if ((threadIdx.x & 63) == 0 && v.stamps)                                             \
+      atomicMax(reinterpret_cast<unsigned long long*>(v.stamps + 8 * (int64_t)blockIdx.x + (k)), \
+                (unsigned long long)__builtin_amdgcn_s_memrealtime());                   \
+  } while (0)
 #else
 #define STAMP(k) do {} while (0)
 #define STAMP_END() do {} while (0)
+#define STAMP_MAX(k) do {} while (0)
 #endif
 
 // 32-bit words per cell set of the teacher's BFS (craft_teach.h: the band of grid columns
@@ -105,6 +114,30 @@ __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F, int obs
   l.bytes = l.ctrl + 16;
   return l;
 }
+
+// The tile kernel's dynamic LDS.  With compact staging (cpt, 5x5 / 7x7 windows) the "obs" piece
+// holds the tile's compact records [tile][RS] words and then the group descriptors [F / 4] u64
+// (craft_obs.h) instead of the u8 rows [tile][F]: 57 words for a 5x5 row of 1076 bytes.
+__host__ __device__ inline int compact_tail_words(int K) { return (K + 5 + 3) / 4; }
+__host__ __device__ inline int compact_stride(int win, int K) {
+  return (2 * win * win + compact_tail_words(K) + 1) | 1;        // + 1 word read past the tail; odd
+}
+__host__ __device__ inline int compact_obs_bytes(int tile, int win, int K, int F) {
+  return ((tile * compact_stride(win, K) * 4 + 15) & ~15) + (F / 4) * 8;
+}
+__host__ __device__ inline LdsLayout tile_lds_layout(int tile, int GS, int F, bool cpt, int win, int K) {
+  if (!cpt) return lds_layout(tile, GS, F);
+  // the same carve with the compact piece in place of the rows: lds_layout's obs size is tile * F
+  // rounded up to 16, so pass an F' that reproduces the compact piece's size exactly
+  const int ob = compact_obs_bytes(tile, win, K, F);
+  LdsLayout l = lds_layout(tile, GS, 0);
+  const int shift = (ob + 15) & ~15;
+  l.inv += shift; l.task += shift; l.rc += shift; l.agent += shift; l.ctrl += shift; l.bytes += shift;
+  return l;
+}
+// Whether a handle's tile kernels use compact staging: 5x5 / 7x7 windows, rows a whole number of
+// 4-value groups (F % 4 == 0) and K >= 4 (a group then spans at most two record words).
+__host__ __device__ inline bool compact_ok(int win, int K, int F) { return win >= 5 && F % 4 == 0 && K >= 4; }
 
 struct TileArgs {
   const int32_t* src;

@@ -190,6 +190,212 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
   }
 }
 
+// ---- compact staging (5x5 / 7x7 windows, the tile kernel) ------------------------------------
+// A 5x5 features() row is 1076 bytes, so 64 u8 rows (69 KB) leave room for two tile workgroups
+// per CU and 65,536 envs run in two rounds.  Instead each env stages a record of RS words:
+//   [0, W2)        local cell c = i*WIN + j: bit k set iff the cell holds kind k (k > 0)
+//   [W2, 2*W2)     pooled block b = bi*WIN + bj: bit k set iff some cell of the block holds k
+//   [2*W2, +TW)    the row's tail as bytes: inventory counts [K], dir one-hot [4], the 0
+//   (+ padding: one word past the tail is read, never used)
+// and E reads each group of 4 consecutive features off it through a per-row descriptor table
+// (the same for every env).  Feature f < 2*W2*K lives at bit f % K of word f / K; a tail feature
+// at byte (f - 2*W2*K) of the tail.  Group q (features 4q .. 4q+3; F % 4 == 0, so groups never
+// straddle rows): bits 0-15 = word w0 of its first feature, then per feature j at 16 + 8j:
+// bit 0 = word w0 + 1 instead of w0, bits 1-5 = shift, bit 6 = a byte (else a bit).  K >= 4, so
+// a group spans at most two words.
+__device__ __forceinline__ void build_group_desc(uint64_t* desc, int W2, int K, int F, int t0, int nthr) {
+  const int L2 = 2 * W2 * K;
+  for (int q = t0; q < F / 4; q += nthr) {
+    int w[4], c[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = 4 * q + j;
+      if (f < L2) {
+        w[j] = f / K;
+        c[j] = (f - w[j] * K) << 1;
+      } else {
+        const int b = f - L2;
+        w[j] = 2 * W2 + (b >> 2);
+        c[j] = ((8 * (b & 3)) << 1) | 64;
+      }
+    }
+    uint64_t d = (uint64_t)w[0];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d |= (uint64_t)(c[j] | (w[j] - w[0])) << (16 + 8 * j);
+    desc[q] = d;
+  }
+}
+
+// The 4 feature values of group `d` of the record at rec_e, one byte each.
+__device__ __forceinline__ uint32_t group_bytes(const uint32_t* rec_e, uint64_t d) {
+  const uint32_t* r = rec_e + (uint32_t)(d & 0xffffu);
+  const uint32_t a0 = r[0], a1 = r[1];               // one ds_read2_b32
+  const uint32_t hi = (uint32_t)(d >> 16);
+  uint32_t out = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t c = (hi >> (8 * j)) & 0xffu;
+    const uint32_t w = (c & 1u) ? a1 : a0;
+    out |= ((w >> ((c >> 1) & 31u)) & ((c & 64u) ? 0xffu : 1u)) << (8 * j);
+  }
+  return out;
+}
+
+// Phase D with compact records, one env split over P lanes (as scatter_env_part): unit 0 writes
+// the local cell masks and the tail words; unit 1 + c ORs grid column c of the pooled window into
+// its blocks' masks (LDS atomics: the columns of one block share a word).  The pooled words must
+// be zero beforehand.
+template <int WIN, int P>
+__device__ __forceinline__ void scatter_env_compact(const SimView& v, const uint8_t* g, const uint8_t* iv,
+                                                    uint32_t ag, uint32_t* rec, int part) {
+  const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+  const int W = v.W, H = v.H, K = v.K;
+  constexpr int W2 = WIN * WIN, hw = WIN / 2, bh = W2 / 2;
+  constexpr int NR = W2 < CRAFT_MAX_DIM ? W2 : CRAFT_MAX_DIM;
+  const int cxa = max(x - bh, 0), cxb = min(x - bh + W2 - 1, W - 1);
+  const int cya = max(y - bh, 0), cyb = min(y - bh + W2 - 1, H - 1);
+  const int nc = cxb - cxa + 1;
+#pragma unroll 1
+  for (int unit = part; unit <= nc; unit += P) {
+    if (unit == 0) {
+      int kk[W2];
+#pragma unroll
+      for (int i = 0; i < WIN; ++i)
+#pragma unroll
+        for (int j = 0; j < WIN; ++j) {
+          const int cx = x - hw + i, cy = y - hw + j;
+          const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
+          const int k = g[min(max(cx, 0), W - 1) * H + min(max(cy, 0), H - 1)];
+          kk[i * WIN + j] = ok ? k : 0;
+        }
+#pragma unroll
+      for (int c = 0; c < W2; ++c) rec[c] = kk[c] ? (1u << kk[c]) : 0u;
+      // the tail: inventory bytes [0, K), dir one-hot [K, K + 4), then zeros
+      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);
+      uint32_t w[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[q] = ivw[q];
+      const int TW = compact_tail_words(K);
+#pragma unroll 1
+      for (int t = 0; t < TW; ++t) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int i = 4 * t + b;
+          uint32_t wi = 0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) wi = (q == (i >> 2)) ? w[q] : wi;
+          const uint32_t inv_b = (wi >> (8 * (i & 3))) & 0xffu;
+          const uint32_t val = i < K ? inv_b : (i - K == dir ? 1u : 0u);   // i - K == 4: the 0
+          o |= val << (8 * b);
+        }
+        rec[2 * W2 + t] = o;
+      }
+    } else {
+      const int cx = cxa + unit - 1;
+      const int bi = (cx - x + bh) / WIN;
+      const uint8_t* col = g + cx * H;
+      int kk[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) kk[j] = col[min(cya + j, H - 1)];
+      uint32_t m[WIN];
+#pragma unroll
+      for (int b = 0; b < WIN; ++b) m[b] = 0;
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int cy = cya + j;
+        const uint32_t bit = (cy <= cyb && kk[j]) ? (1u << kk[j]) : 0u;
+        const int bj = (cy - y + bh) / WIN;
+#pragma unroll
+        for (int b = 0; b < WIN; ++b) m[b] |= (b == bj) ? bit : 0u;
+      }
+      uint32_t* brow = rec + W2 + bi * WIN;
+#pragma unroll
+      for (int b = 0; b < WIN; ++b)
+        if (m[b]) atomicOr(brow + b, m[b]);
+    }
+  }
+}
+
+template <int WIN, int TILE, int NTHR = kThreads>
+__device__ __forceinline__ void scatter_compact(const SimView& v, const uint8_t* s_grid, const uint8_t* s_inv,
+                                                const uint32_t* s_agent, uint32_t* s_rec, int RS, int nE, int tid) {
+  constexpr int kParts = NTHR / TILE;
+  const int e = tid % TILE, part = tid / TILE;
+  const uint32_t ag = s_agent[e];
+  if (e < nE && (ag >> 24))
+    scatter_env_compact<WIN, kParts>(v, s_grid + e * v.GS, s_inv + e * kInvStride, ag, s_rec + e * RS, part);
+}
+
+// 16 bytes of output from four packed feature-byte words (as pack16 on the u8 rows).
+template <int FMT>
+__device__ __forceinline__ obs_vec pack_bytes(const uint32_t* b) {
+  if (FMT == CRAFT_OBS_F32) {
+    const uint32_t w = b[0];
+    return obs_vec{__float_as_uint((float)(w & 0xff)), __float_as_uint((float)((w >> 8) & 0xff)),
+                   __float_as_uint((float)((w >> 16) & 0xff)), __float_as_uint((float)(w >> 24))};
+  } else if (FMT == CRAFT_OBS_BF16) {
+    auto bf = [](uint32_t x) { return __float_as_uint((float)x) >> 16; };
+    auto two = [&](uint32_t x) { return bf(x & 0xff) | (bf((x >> 8) & 0xff) << 16); };
+    return obs_vec{two(b[0]), two(b[0] >> 16), two(b[1]), two(b[1] >> 16)};
+  } else {
+    return obs_vec{b[0], b[1], b[2], b[3]};
+  }
+}
+
+// Phase E with compact records: the tile's rows as one flat stream of 16-byte stores (as
+// stream_obs), each store's 4 / 8 / 16 values read off the records by group descriptor.
+template <int FMT, int NTHR = kThreads>
+__device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint64_t* s_desc, void* obs,
+                                               int64_t env0, int F, int RS, int nE, int policy, int tid) {
+  constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
+  constexpr int PER = 16 / ESZ;                // values per 16-byte store
+  constexpr int GPS = PER / 4;                 // groups per store
+  const int G = F >> 2;                        // groups per row
+  const int total = nE * F;
+  const int nv = total / PER;
+  const float invG = 1.0f / (float)G;
+  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
+  constexpr int U = 4;
+  for (int base = tid; base < nv; base += U * NTHR) {
+    obs_vec o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sidx = base + u * NTHR;
+      if (sidx < nv) {
+        uint32_t b[GPS];
+#pragma unroll
+        for (int j = 0; j < GPS; ++j) {
+          const int gg = sidx * GPS + j;
+          int e = (int)((float)gg * invG);       // then corrected: exact for any tile
+          e -= (e * G > gg) ? 1 : 0;
+          e += ((e + 1) * G <= gg) ? 1 : 0;
+          const int q = gg - e * G;
+          b[j] = group_bytes(s_rec + e * RS, s_desc[q]);
+        }
+        o[u] = pack_bytes<FMT>(b);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sidx = base + u * NTHR;
+      if (sidx < nv) {
+        if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 2);         // nt
+        else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 16);   // sc1
+        else __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 0);
+      }
+    }
+  }
+  for (int f = nv * PER + tid; f < total; f += NTHR) {       // the last few values of the tile
+    const int e = f / F, ff = f - e * F;
+    const uint32_t bt = (group_bytes(s_rec + e * RS, s_desc[ff >> 2]) >> (8 * (ff & 3))) & 0xffu;
+    if (FMT == CRAFT_OBS_F32) reinterpret_cast<float*>(tile_out)[f] = (float)bt;
+    else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint16_t*>(tile_out)[f] = (uint16_t)(__float_as_uint((float)bt) >> 16);
+    else tile_out[f] = (uint8_t)bt;
+  }
+}
+
 // Phase D: all threads scatter the non-zero bytes of each env's features() row
 // into the zeroed u8 rows s_obs[TILE][F] (scatter_env_part, NTHR / TILE threads per
 // env).  s_agent[e] = x | y<<8 | dir<<16 | 1<<24 for a live env (0 = skip).

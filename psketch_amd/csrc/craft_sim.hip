@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "craft_device.h"
+#include "craft_host.h"
 
 namespace craft {
 hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
@@ -147,6 +148,7 @@ struct craft_sim {
   int32_t* d_err = nullptr;
   SimView view{};
   int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
+  int tile_knob = 0;                // craft_sim_tune's tile_envs (0 = each kernel's default)
   int resident_cap = 0;             // 0: no cap on tile workgroups per CU
   int rollout_chunk = 0;            // craft_rollout ticks per work unit (0: the whole launch)
   int rollout_threads = 0;          // craft_rollout threads per tile workgroup (0: 8 per env)
@@ -180,49 +182,13 @@ int hip_fail(craft_sim* sim, hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail((sim), _e, #expr); \
   } while (0)
 
-int validate_config(const craft_config_t* c, std::string& msg) {
-  if (c->abi_version != CRAFT_ABI_VERSION) { msg = "abi_version mismatch"; return CRAFT_EINVAL; }
-  if (c->width < 3 || c->height < 3 || c->width > CRAFT_MAX_DIM || c->height > CRAFT_MAX_DIM ||
-      c->width * c->height > CRAFT_MAX_CELLS) { msg = "WIDTH/HEIGHT out of range (3..16)"; return CRAFT_EINVAL; }
-  if (c->window_width != c->window_height ||
-      (c->window_width != 3 && c->window_width != 5 && c->window_width != 7)) {
-    msg = "WINDOW_WIDTH == WINDOW_HEIGHT in {3,5,7} required"; return CRAFT_EINVAL;
-  }
-  if (c->n_kinds < 2 || c->n_kinds > CRAFT_MAX_KINDS) { msg = "n_kinds out of range"; return CRAFT_EINVAL; }
-  const int ww = c->window_width;
-  if (c->n_features != 2 * ww * ww * c->n_kinds + c->n_kinds + 5) {
-    msg = "n_features != 2*ww*wh*n_kinds + n_kinds + 5 (craft.py:69-75)"; return CRAFT_EINVAL;
-  }
-  if (c->max_timesteps < 1 || c->max_timesteps > 255) { msg = "max_timesteps must be 1..255"; return CRAFT_EINVAL; }
-  if (c->bridge_kind <= 0 || c->bridge_kind >= c->n_kinds || c->axe_kind <= 0 || c->axe_kind >= c->n_kinds) {
-    msg = "bridge/axe kind out of range"; return CRAFT_EINVAL;
-  }
-  for (int k = 0; k < CRAFT_MAX_KINDS; ++k)
-    if (c->kind_class[k] > CRAFT_KIND_STONE) { msg = "bad kind_class"; return CRAFT_EINVAL; }
-  if (c->n_recipes < 0 || c->n_recipes > CRAFT_MAX_RECIPES) { msg = "n_recipes out of range"; return CRAFT_EINVAL; }
-  for (int r = 0; r < c->n_recipes; ++r) {
-    const craft_recipe_t& rc = c->recipe[r];
-    if (rc.output <= 0 || rc.output >= c->n_kinds || rc.workshop <= 0 || rc.workshop >= c->n_kinds ||
-        rc.n_inputs < 1 || rc.n_inputs > CRAFT_MAX_INGREDIENTS) { msg = "bad recipe"; return CRAFT_EINVAL; }
-    if (rc.yield != 1) { msg = "_yield != 1 is not supported (u8 inventory counts)"; return CRAFT_EINVAL; }
-    for (int i = 0; i < rc.n_inputs; ++i)
-      if (rc.input_kind[i] <= 0 || rc.input_kind[i] >= c->n_kinds || rc.input_count[i] < 1 ||
-          rc.input_count[i] > 255) { msg = "bad recipe input"; return CRAFT_EINVAL; }
-  }
-  if (c->n_tasks < 1 || c->n_tasks > CRAFT_MAX_TASKS) { msg = "n_tasks out of range"; return CRAFT_EINVAL; }
-  for (int t = 0; t < c->n_tasks; ++t) {
-    const craft_task_t& tk = c->task[t];
-    if (tk.goal < CRAFT_GOAL_OTHER || tk.goal > CRAFT_GOAL_USE || tk.arg_kind < 0 ||
-        tk.arg_kind >= c->n_kinds || tk.n_subtasks < 0 || tk.n_subtasks > CRAFT_MAX_SUBTASKS) {
-      msg = "bad task"; return CRAFT_EINVAL;
-    }
-    if ((tk.goal == CRAFT_GOAL_GET || tk.goal == CRAFT_GOAL_MAKE || tk.goal == CRAFT_GOAL_GO) && tk.arg_kind == 0) {
-      msg = "get/make/go task without a kind argument"; return CRAFT_EINVAL;
-    }
-    for (int s = 0; s < tk.n_subtasks; ++s)
-      if (tk.subtask[s] < 0 || tk.subtask[s] >= c->n_tasks) { msg = "bad subtask id"; return CRAFT_EINVAL; }
-  }
-  return CRAFT_OK;
+using craft_host::validate_config;
+
+// The tile kernel's default envs per workgroup (craft_sim_create, craft_sim_tune(0, ...)).
+int default_tile(int win, bool cpt) {
+  if (win == 3) return 64;
+  if (win == 5) return cpt ? 64 : 32;
+  return cpt ? 32 : 16;
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -240,12 +206,25 @@ size_t lds_bytes(const craft_sim* s, int tile, int obs_bufs = 1, bool pristine =
   return b;
 }
 
+// The tile kernel's (craft_tile.h): u8 rows, or compact records for 5x5 / 7x7 windows (v.cpt).
+size_t tile_lds_bytes(const craft_sim* s, int tile) {
+  const SimView& v = s->view;
+  size_t b = (size_t)craft::tile_lds_layout(tile, v.GS, v.F, v.cpt != 0, s->cfg.window_width, v.K).bytes;
+  if (s->resident_cap > 0) {
+    const size_t capped = ((size_t)163840 / s->resident_cap) & ~size_t(15);
+    if (capped > b) b = capped;
+  }
+  return b;
+}
+
 // The workgroup shape craft_rollout launches with (craft_sim_rollout_shape).  Default
 // (threads 0): for 3x3 windows the split-producer kernel on 32-env tiles with 6
 // streaming waves (7-15 % faster than 64-env tiles at 65536 envs);
 // otherwise the handle's tile with 256 threads (512 for 64-env tiles).
 void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
-  int t = s->tile, nt = s->rollout_threads;
+  // the rollout kernels stage u8 rows (double-buffered): their default tile keeps ~40 KB per buffer
+  const int win = s->cfg.window_width;
+  int t = s->tile_knob ? s->tile_knob : (win == 3 ? 64 : (win == 5 ? 32 : 16)), nt = s->rollout_threads;
   if (nt == 0 && s->cfg.window_width == 3) {
     t = 32;
     nt = 512;
@@ -286,7 +265,7 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
-  hipError_t e = craft::launch_tile(mode, s->cfg.window_width, s->tile, s->view, a, lds_bytes(s, s->tile),
+  hipError_t e = craft::launch_tile(mode, s->cfg.window_width, s->tile, s->view, a, tile_lds_bytes(s, s->tile),
                                     reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, what);
   return CRAFT_OK;
@@ -296,19 +275,7 @@ int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* 
 
 extern "C" {
 
-const char* craft_strerror(int status) {
-  switch (status) {
-    case CRAFT_OK: return "ok";
-    case CRAFT_EINVAL: return "invalid argument";
-    case CRAFT_EBADACTION: return "Unexpected action";
-    case CRAFT_EINVARIANT: return "impossible world configuration";
-    case CRAFT_ETEACHER: return "teacher assertion";
-    case CRAFT_EHIP: return "HIP runtime error";
-    case CRAFT_ENOMEM: return "out of memory";
-    case CRAFT_ERANGE: return "index out of range";
-    default: return "unknown status";
-  }
-}
+const char* craft_strerror(int status) { return craft_host::status_text(status); }
 
 int craft_host_flag_pointer(void* host, int32_t** device_out) {
   if (!host || !device_out) return CRAFT_EINVAL;
@@ -342,8 +309,13 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   // stats rows: one per 16-env tile, plus the step kernel's last workgroup's tick waves (its
   // wave count is rounded up to the workgroup's 4)
   s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs + 4;
-  // default tile: the observation rows staged in LDS stay near 40 KB per workgroup
-  s->tile = cfg->window_width == 3 ? 64 : (cfg->window_width == 5 ? 32 : 16);
+  // default tile: 64 envs (3x3 rows, 5x5 compact records: ~30 KB, 4 workgroups per CU), 32 for
+  // 7x7 compact records; without compact staging the u8 rows stay near 40 KB per workgroup
+  // (CRAFT_COMPACT=0 at creation: the u8 rows instead, a diagnostic for the A/B and parity tests)
+  const char* cpt_env = getenv("CRAFT_COMPACT");
+  s->view.cpt = craft::compact_ok(cfg->window_width, cfg->n_kinds, cfg->n_features) &&
+                !(cpt_env && atoi(cpt_env) == 0) ? 1 : 0;
+  s->tile = default_tile(cfg->window_width, s->view.cpt != 0);
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
@@ -364,11 +336,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   }
   std::vector<uint16_t> task_tab(CRAFT_MAX_TASKS, 0);
   std::vector<int32_t> task_sub(CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS, 0);
-  for (int t = 0; t < cfg->n_tasks; ++t) {
-    const craft_task_t& tk = cfg->task[t];
-    task_tab[t] = (uint16_t)(tk.goal | (tk.arg_kind << 4) | (tk.n_subtasks << 12));
-    for (int q = 0; q < tk.n_subtasks; ++q) task_sub[CRAFT_MAX_SUBTASKS * t + q] = tk.subtask[q];
-  }
+  craft_host::task_tables(*cfg, task_tab.data(), task_sub.data());
   auto cleanup = [&](hipError_t e, const char* what) {
     fprintf(stderr, "craft_sim_create: %s: %s\n", what, hipGetErrorString(e));
     craft_sim_destroy(s);
@@ -441,7 +409,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
 
 int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_cu, int32_t obs_store) {
   if (!s) return CRAFT_EINVAL;
-  if (tile_envs == 0) tile_envs = s->cfg.window_width == 3 ? 64 : (s->cfg.window_width == 5 ? 32 : 16);
+  s->tile_knob = tile_envs;
+  if (tile_envs == 0) tile_envs = default_tile(s->cfg.window_width, s->view.cpt != 0);
   if (tile_envs != 16 && tile_envs != 32 && tile_envs != 64)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune: tile_envs must be 16, 32 or 64");
   if (max_resident_per_cu != 0 && (max_resident_per_cu < 3 || max_resident_per_cu > 32))
@@ -566,55 +535,15 @@ int craft_sim_error_word(craft_sim_t* s, int32_t* out, void* stream) {
 int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t count) {
   if (!s || !grids || first < 0 || count < 0) return fail(s, CRAFT_EINVAL, "craft_pool_load: bad argument");
   if ((int64_t)first + count > s->pool_capacity) return fail(s, CRAFT_ERANGE, "craft_pool_load: beyond pool capacity");
-  const int W = s->cfg.width, H = s->cfg.height, C = W * H, CS = s->view.CS;
+  const int C = s->cfg.width * s->cfg.height, CS = s->view.CS;
   std::vector<uint8_t> staged((size_t)count * CS, 0);
   std::vector<uint8_t> conn((size_t)count, 0);
-  // Kinds a border cell may hold: occupied, inert under USE (never cleared, so the agent never
-  // reaches the border) and no task's target.  The teacher's band-layout BFS drops columns 0 and
-  // W-1 (craft_teach.h) and the kernels never index past the ring; make_data.py:108-112 and
-  // sample_scenario (craft.py:129-133) fill the ring with `boundary`, which qualifies.
-  uint32_t border_ok = 0;
-  for (int k = 1; k < s->cfg.n_kinds && k < 32; ++k)
-    if (s->cfg.kind_class[k] == CRAFT_KIND_INERT) border_ok |= 1u << k;
-  for (int t = 0; t < s->cfg.n_tasks; ++t)
-    if (s->cfg.task[t].arg_kind > 0 && s->cfg.task[t].arg_kind < 32) border_ok &= ~(1u << s->cfg.task[t].arg_kind);
   for (int p = 0; p < count; ++p) {
     const uint8_t* g = grids + (size_t)p * C;
-    for (int c = 0; c < C; ++c) {
-      if (g[c] >= s->cfg.n_kinds)
-        return fail(s, CRAFT_EINVARIANT, "craft_pool_load: kind id out of range in grid " + std::to_string(first + p));
-      const int x = c / H, y = c % H;
-      if ((x == 0 || y == 0 || x == W - 1 || y == H - 1) && !((border_ok >> g[c]) & 1u))
-        return fail(s, CRAFT_EINVARIANT, "craft_pool_load: grid " + std::to_string(first + p) + " border cell (" +
-                                             std::to_string(x) + ", " + std::to_string(y) + ") holds kind " +
-                                             std::to_string(g[c]) +
-                                             ": the ring must be occupied by inert, non-target kinds "
-                                             "(make_data.py:108-112 builds a boundary ring)");
-    }
+    std::string msg;
+    const int rc = craft_host::check_pool_grid(s->cfg, g, (int64_t)first + p, msg, &conn[p]);
+    if (rc) return fail(s, rc, msg);
     std::memcpy(staged.data() + (size_t)p * CS, g, C);
-    // are the free cells one 4-connected component?  Cells are only ever cleared next to the
-    // agent, so every env grid of this scenario then keeps its free cells connected, and the
-    // teacher reads target reachability off the grid instead of flooding it (craft_teach.h)
-    std::vector<int> stack;
-    std::vector<uint8_t> seen(C, 0);
-    int n_free = 0, first_free = -1;
-    for (int c = 0; c < C; ++c)
-      if (g[c] == 0) { ++n_free; if (first_free < 0) first_free = c; }
-    int n_seen = 0;
-    if (first_free >= 0) { stack.push_back(first_free); seen[first_free] = 1; }
-    while (!stack.empty()) {
-      const int c = stack.back();
-      stack.pop_back();
-      ++n_seen;
-      const int x = c / H, y = c % H;
-      const int nb[4][2] = {{x, y - 1}, {x, y + 1}, {x - 1, y}, {x + 1, y}};
-      for (auto& q : nb) {
-        if (q[0] < 0 || q[0] >= W || q[1] < 0 || q[1] >= H) continue;
-        const int d = q[0] * H + q[1];
-        if (!seen[d] && g[d] == 0) { seen[d] = 1; stack.push_back(d); }
-      }
-    }
-    conn[p] = n_seen == n_free ? 1 : 0;
   }
   HIP_TRY(s, hipSetDevice(s->device));
   if (count) {
@@ -732,7 +661,8 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
     e = craft::launch_tick2(tl, nw, s->view, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
   } else {
     const int tile = craft::kMaxTileEnvs;
-    const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
+    const size_t lds = (size_t)craft::tile_lds_layout(tile, s->view.GS, s->view.F, s->view.cpt != 0,
+                                                      s->cfg.window_width, s->view.K).bytes + tile * 4 +
                        CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16;   // + task | frozen words, task_sub, D sync
     e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, s->view, a, lds, st);
   }

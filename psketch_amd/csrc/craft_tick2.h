@@ -77,6 +77,10 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t envw = (int64_t)blockIdx.x * (J * kTick2Tile);          // this workgroup's first env
+  // CRAFT_STAMPS builds (tools/tick2_stamps.py): 0 start, 1 wave 0's loads landed, 2 wave 0's C
+  // done, 3 past the barrier, 4 wave 0's first store issued, 5 the last tick wave done issuing
+  // stores, 6 the last teacher wave done, 7 the XCC
+  STAMP(0);
   const bool want_obs = a.obs != nullptr;
   auto tile_envs = [&](int j) { return (int)max((int64_t)0, min((int64_t)kTick2Tile, a.n - envw - j * kTick2Tile)); };
 
@@ -155,6 +159,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP(1);
 
     uint32_t* ivw = reinterpret_cast<uint32_t*>(s_inv + le * kInvStride);
     uint8_t* iv = s_inv + le * kInvStride;
@@ -244,6 +249,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       atomicAdd(r + 2, (unsigned long long)__popcll(bt));
       if (a.any_live && bl) *a.any_live = 1;                             // idempotent plain store
     }
+    STAMP(2);
   } else if (want_obs && wave < kTick2Waves) {
     // waves J..3: zero the observation rows of every tick wave
     uint4* z = reinterpret_cast<uint4*>(smem + lay.obs);
@@ -252,6 +258,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   }
   if (TL == 0 && !want_obs) return;                                      // no barrier follows
   __syncthreads();
+  STAMP(3);
 
   if (wave < kTick2Waves) {
     if (!want_obs) return;
@@ -267,6 +274,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (j == 0) STAMP(4);
       switch (v.obs_fmt) {
         case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
         case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
@@ -276,6 +284,14 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    STAMP_MAX(5);
+#ifdef CRAFT_STAMPS
+    if (tid == 0 && v.stamps) {
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      v.stamps[8 * (int64_t)blockIdx.x + 7] = xcc;
+    }
+#endif
     return;
   }
 
@@ -307,6 +323,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       }
       if (ql == 0) a.label[i] = action;
     }
+    STAMP_MAX(6);
   }
 }
 

@@ -36,7 +36,9 @@ class CraftSim:
     world: a gamedef.WORLDS name ("craft_medium_12x12" is the benchmark world),
     a configs/worlds YAML path or a dict.  recipes / hints: YAML paths or None
     for the built-in tables.  env_id_base: global id of slot 0 (rank * N when
-    sharded), which keys every per-env random draw.
+    sharded), which keys every per-env random draw.  device: a GPU index (default:
+    the current one) runs the HIP library; device="cpu" runs the CPU variant of the
+    same ABI (libpsketch_craft_cpu.so) on host tensors, the same results bit for bit.
     """
 
     def __init__(self, world="craft_medium_12x12", n_envs=4096, device=None, env_id_base=0,
@@ -45,6 +47,10 @@ class CraftSim:
         if device is None:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if self.device.type not in ("cuda", "cpu"):
+            raise ValueError(f"device {self.device}: a GPU index or 'cpu'")
+        self._cpu = self.device.type == "cpu"
+        self._L = N.lib(cpu=self._cpu)
         self.params = world_params(world)
         self.cookbook = Cookbook(recipes)
         self.task_manager = TaskManager(hints)
@@ -57,9 +63,9 @@ class CraftSim:
         self.pool_capacity = int(pool_capacity)
         self.pool_count = 0
         handle = ctypes.c_void_p()
-        N.check(N.lib().craft_sim_create(ctypes.byref(self.config), self.device.index, self.n_envs,
+        N.check(self._L.craft_sim_create(ctypes.byref(self.config), self.device.index or 0, self.n_envs,
                                          self.env_id_base, self.pool_capacity,
-                                         ctypes.byref(handle)), what="craft_sim_create")
+                                         ctypes.byref(handle)), what="craft_sim_create", L=self._L)
         self._h = handle
         self.obs_format, self.obs_dtype = "f32", torch.float32
         self._rollout_cache = None
@@ -68,7 +74,7 @@ class CraftSim:
     def close(self):
         self._rollout_cache = None
         if getattr(self, "_h", None):
-            N.lib().craft_sim_destroy(self._h)
+            self._L.craft_sim_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -80,7 +86,7 @@ class CraftSim:
     def tune(self, tile_envs=0, max_resident_per_cu=0, obs_store=0):
         """Tile-kernel geometry and observation-store cache policy (0 write-back,
         1 nontemporal, 2 write-through); results are identical for every setting."""
-        self._check(N.lib().craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu),
+        self._check(self._L.craft_sim_tune(self._h, int(tile_envs), int(max_resident_per_cu),
                                            int(obs_store)), "craft_sim_tune")
 
     def tune_rollout(self, chunk_ticks=0, threads=0):
@@ -88,20 +94,20 @@ class CraftSim:
         launch, the default; -1 = one continuous pipeline per workgroup across
         its tiles) and threads per tile workgroup (0 = the library's default
         shape); results are identical for every setting."""
-        self._check(N.lib().craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
+        self._check(self._L.craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
                     "craft_sim_tune_rollout")
 
     def tune_teach(self, kernel=0):
         """Which kernel step(..., labels=) launches (craft_sim_tune_teach): 0 the
         measured best, 1 the one-tile kernel, 2 the two-tile kernel (3x3 windows); results
         are identical for every setting."""
-        self._check(N.lib().craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
+        self._check(self._L.craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
 
     def step_shape(self, teach=False):
         """(kernel name, envs per tile / workgroup, teacher lanes per env) that step()
         launches, without (teach=False) or with labels= (craft_sim_step_shape)."""
         k, e, l = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-        self._check(N.lib().craft_sim_step_shape(self._h, int(bool(teach)), ctypes.byref(k),
+        self._check(self._L.craft_sim_step_shape(self._h, int(bool(teach)), ctypes.byref(k),
                                                  ctypes.byref(e), ctypes.byref(l)),
                     "craft_sim_step_shape")
         return N.KERNEL_NAMES[k.value], e.value, l.value
@@ -110,14 +116,14 @@ class CraftSim:
         """(tile_envs, threads, split) the next rollout() launches with, as the
         library resolves its knobs (craft_sim_rollout_shape)."""
         t, nt, sp = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-        self._check(N.lib().craft_sim_rollout_shape(self._h, ctypes.byref(t), ctypes.byref(nt),
+        self._check(self._L.craft_sim_rollout_shape(self._h, ctypes.byref(t), ctypes.byref(nt),
                                                     ctypes.byref(sp)), "craft_sim_rollout_shape")
         return t.value, nt.value, bool(sp.value)
 
     def tile_shape(self):
         """(tile_envs, obs_store) of the tick kernel (craft_sim_tile_shape)."""
         t, st = ctypes.c_int32(), ctypes.c_int32()
-        self._check(N.lib().craft_sim_tile_shape(self._h, ctypes.byref(t), ctypes.byref(st)),
+        self._check(self._L.craft_sim_tile_shape(self._h, ctypes.byref(t), ctypes.byref(st)),
                     "craft_sim_tile_shape")
         return t.value, st.value
 
@@ -128,23 +134,26 @@ class CraftSim:
         """Element type of every observation this simulator writes: "f32"
         (default), "bf16" or "u8" — the same exact integer values in each."""
         code, dtype = self._OBS_FORMATS[fmt]
-        self._check(N.lib().craft_sim_set_obs_format(self._h, code), "craft_sim_set_obs_format")
+        self._check(self._L.craft_sim_set_obs_format(self._h, code), "craft_sim_set_obs_format")
         self.obs_format, self.obs_dtype = fmt, dtype
         self._rollout_cache = None
 
     def _stream(self):
         # the raw hipStream_t of the caller's current stream on this device (an int; the C ABI's
-        # argtypes take it as void*): ~5x cheaper than building a torch.cuda.Stream object
+        # argtypes take it as void*): ~5x cheaper than building a torch.cuda.Stream object.  The
+        # CPU variant ignores it.
+        if self._cpu:
+            return None
         return torch._C._cuda_getCurrentRawStream(self.device.index)
 
     def _check(self, status, what):
-        N.check(status, self._h, what)
+        N.check(status, self._h, what, L=self._L)
 
     def check(self):
         """Synchronises and raises if a kernel latched an error (bad action,
         teacher assertion, out-of-range slot)."""
         slot = ctypes.c_int64(-1)
-        self._check(N.lib().craft_sim_check(self._h, ctypes.byref(slot), self._stream()),
+        self._check(self._L.craft_sim_check(self._h, ctypes.byref(slot), self._stream()),
                     "kernel error")
 
     def error_word(self, out=None):
@@ -153,7 +162,7 @@ class CraftSim:
         if out is None:
             out = torch.empty(4, dtype=torch.int32, device=self.device)
         self._buf("out", out, torch.int32, (4,))
-        self._check(N.lib().craft_sim_error_word(self._h, _ptr(out), self._stream()),
+        self._check(self._L.craft_sim_error_word(self._h, _ptr(out), self._stream()),
                     "craft_sim_error_word")
         return out
 
@@ -201,7 +210,7 @@ class CraftSim:
         """grids: uint8 [P, W, H] or [P, W*H] kind ids (x-major), host or device."""
         g = np.ascontiguousarray(np.asarray(torch.as_tensor(grids).cpu(), dtype=np.uint8))
         g = g.reshape(g.shape[0], self.width * self.height)
-        self._check(N.lib().craft_pool_load(self._h, g.ctypes.data_as(ctypes.c_void_p), int(first),
+        self._check(self._L.craft_pool_load(self._h, g.ctypes.data_as(ctypes.c_void_p), int(first),
                                             int(g.shape[0])), "craft_pool_load")
         self.pool_count = max(self.pool_count, first + g.shape[0])
 
@@ -223,7 +232,7 @@ class CraftSim:
                         dtype=np.int32)
         out = torch.empty((count, 2), dtype=torch.int32, device=self.device) if init_pos else None
         sid0 = first if scenario_id0 is None else scenario_id0
-        self._check(N.lib().craft_pool_generate(
+        self._check(self._L.craft_pool_generate(
             self._h, ctypes.c_uint64(seed & (2**64 - 1)), int(sid0), int(first), int(count),
             self.cookbook.index["boundary"], prims.ctypes.data_as(ctypes.c_void_p), len(prims),
             self.params["N_PRIMITIVES"], ws.ctypes.data_as(ctypes.c_void_p), len(ws), _ptr(out),
@@ -236,7 +245,7 @@ class CraftSim:
         n = self.n_envs
         args = [self._i32(a, n) for a in (scenario, pos_x, pos_y, dir, task)]
         self._args_keepalive = args
-        self._check(N.lib().craft_reset(self._h, *[_ptr(a) for a in args], self._obs(obs), self._stream()),
+        self._check(self._L.craft_reset(self._h, *[_ptr(a) for a in args], self._obs(obs), self._stream()),
                     "craft_reset")
         return obs
 
@@ -260,7 +269,7 @@ class CraftSim:
             r = self._buf("reward", reward, torch.float32, (n,))
             d = self._buf("done", done, torch.uint8, (n,))
             sc = self._buf("success", success, torch.int8, (n,))
-            self._check(N.lib().craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
+            self._check(self._L.craft_step(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
                                            int(tick), flags, self._obs(obs), _ptr(r),
                                            _ptr(d), _ptr(sc), self._stream()), "craft_step")
             return obs
@@ -294,10 +303,10 @@ class CraftSim:
         args.flags = flags
         if labels is not None:
             self._buf("labels", labels, torch.int32, (n,))
-            self._check(N.lib().craft_step_teach(self._h, ctypes.byref(args), _ptr(labels),
+            self._check(self._L.craft_step_teach(self._h, ctypes.byref(args), _ptr(labels),
                                                  self._stream()), "craft_step_teach")
         else:
-            self._check(N.lib().craft_step_ex(self._h, ctypes.byref(args), self._stream()),
+            self._check(self._L.craft_step_ex(self._h, ctypes.byref(args), self._stream()),
                         "craft_step")
         return obs
 
@@ -338,7 +347,7 @@ class CraftSim:
         a = None
         if actions is not None:
             a = self._i32(actions, n * n_ticks)
-        self._rollout_fn = N.lib().craft_rollout
+        self._rollout_fn = self._L.craft_rollout
         self._check(self._rollout_fn(self._h, _ptr(a), ctypes.c_uint64(seed & (2**64 - 1)),
                                      int(tick0), int(n_ticks),
                                      N.STEP_AUTORESET if autoreset else 0, _ptr(obs),
@@ -362,7 +371,7 @@ class CraftSim:
         """Device int64[3] {successes, episodes ended, env-steps}."""
         if out is None:
             out = torch.zeros(3, dtype=torch.int64, device=self.device)
-        self._check(N.lib().craft_stats(self._h, _ptr(out), int(bool(reset)), self._stream()),
+        self._check(self._L.craft_stats(self._h, _ptr(out), int(bool(reset)), self._stream()),
                     "craft_stats")
         return out
 
@@ -374,7 +383,7 @@ class CraftSim:
         n = a.numel()
         s, d = self._i32(src, n), self._i32(dst, n)
         self._buf("codes", codes, torch.int8, (n,))
-        self._check(N.lib().craft_transition(self._h, _ptr(s), _ptr(d), _ptr(a), n, _ptr(codes),
+        self._check(self._L.craft_transition(self._h, _ptr(s), _ptr(d), _ptr(a), n, _ptr(codes),
                                              self._stream()), "craft_transition")
         return codes
 
@@ -383,7 +392,7 @@ class CraftSim:
         n = s.numel() if s is not None else (self.n_envs if n is None else n)
         t = self._i32(tasks, n)
         self._buf("sat", sat, torch.int8, (n,))
-        self._check(N.lib().craft_observe(self._h, _ptr(s), n, _ptr(t), self._obs(obs, n), _ptr(sat),
+        self._check(self._L.craft_observe(self._h, _ptr(s), n, _ptr(t), self._obs(obs, n), _ptr(sat),
                                           self._stream()), "craft_observe")
         return obs, sat
 
@@ -395,7 +404,7 @@ class CraftSim:
             action_out = torch.empty(n, dtype=torch.int32, device=self.device)
         self._buf("action_out", action_out, torch.int32, (n,))
         self._buf("path_len_out", path_len_out, torch.int32, (n,))
-        self._check(N.lib().craft_teacher(self._h, _ptr(s), n, _ptr(t), _ptr(action_out),
+        self._check(self._L.craft_teacher(self._h, _ptr(s), n, _ptr(t), _ptr(action_out),
                                           _ptr(path_len_out), self._stream()), "craft_teacher")
         return action_out, path_len_out
 
@@ -408,7 +417,7 @@ class CraftSim:
         shapes = {"agent": ((n, 4), torch.int32), "inventory": ((n, self.n_kinds), torch.int32),
                   "grid": ((n, self.width * self.height), torch.uint8), "spec": ((n, 5), torch.int32)}
         out = {f: torch.empty(shapes[f][0], dtype=shapes[f][1], device=dev) for f in fields}
-        self._check(N.lib().craft_get_state(self._h, _ptr(s), n, _ptr(out.get("agent")),
+        self._check(self._L.craft_get_state(self._h, _ptr(s), n, _ptr(out.get("agent")),
                                             _ptr(out.get("inventory")), _ptr(out.get("grid")),
                                             _ptr(out.get("spec")), self._stream()), "craft_get_state")
         return out
@@ -419,7 +428,7 @@ class CraftSim:
         ag = self._i32(agent)
         iv = self._i32(inventory)
         s = self._i32(slots, n)
-        self._check(N.lib().craft_set_state(self._h, _ptr(s), n, _ptr(sp), _ptr(ag), _ptr(iv),
+        self._check(self._L.craft_set_state(self._h, _ptr(s), n, _ptr(sp), _ptr(ag), _ptr(iv),
                                             self._stream()), "craft_set_state")
 
 

@@ -21,13 +21,25 @@ def header_functions():
     return sorted(set(re.findall(r"\b(craft_[a-z_]+)\s*\(", src)))
 
 
-def test_library_exports_every_header_symbol():
-    lib = N.lib()
+@pytest.mark.parametrize("cpu", [False, True])
+def test_library_exports_every_header_symbol(cpu):
+    """The HIP library and its CPU variant export every entry point
+    include/craft.h declares, and the ctypes table binds exactly those."""
+    lib = N.lib(cpu=cpu)
     names = header_functions()
     assert len(names) >= 15
     for name in names:
         assert hasattr(lib, name), name
     assert sorted(N.SIGNATURES) == names
+
+
+def test_create_rejects_bad_config_on_both_libraries():
+    for cpu in (False, True):
+        _, _, _, cfg = make_tables()
+        cfg.n_features += 1
+        h = ctypes.c_void_p()
+        assert N.lib(cpu=cpu).craft_sim_create(ctypes.byref(cfg), 0, 16, 0, 4, ctypes.byref(h)) == N.EINVAL
+        assert not h.value
 
 
 def test_config_layout_matches_c(oracle_mod):

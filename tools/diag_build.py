@@ -1,0 +1,38 @@
+"""Diagnostic library builder (never the product): psketch_amd/lib/libpsketch_craft_diag.so, linked
+from the product's objects except the named translation units, which are compiled again with
+-DCRAFT_STAMPS (s_memrealtime phase stamps, craft_device.h) and any extra defines.
+
+    python tools/diag_build.py craft_sim craft_tile [-DNAME ...]"""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import __graft_entry__ as ge  # noqa: E402
+
+DIAG = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_diag.so")
+
+
+def build(stamped=("craft_sim", "craft_tile"), defines=()):
+    ge.build()
+    obj = os.path.join(REPO, "psketch_amd", "lib", "obj")
+    dobj = os.path.join(REPO, "psketch_amd", "lib", "obj_diag")
+    os.makedirs(dobj, exist_ok=True)
+    objs = []
+    for src in ge.SOURCES:
+        base = os.path.splitext(src)[0]
+        if base in stamped:
+            o = os.path.join(dobj, base + ".o")
+            subprocess.check_call([ge.HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                                   "-DCRAFT_STAMPS", *defines, "-c", os.path.join(ge.CSRC, src), "-o", o])
+        else:
+            o = os.path.join(obj, base + ".o")
+        objs.append(o)
+    subprocess.check_call([ge.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", DIAG] + objs)
+    return DIAG
+
+
+if __name__ == "__main__":
+    names = [a for a in sys.argv[1:] if not a.startswith("-D")]
+    build(tuple(names) or ("craft_sim", "craft_tile"), [a for a in sys.argv[1:] if a.startswith("-D")])

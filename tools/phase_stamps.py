@@ -11,8 +11,8 @@ import __graft_entry__ as ge
 DIAG = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_diag.so")
 if "--build" in sys.argv:          # the tile kernel and craft_sim stamped, every other object the product's
     sys.path.insert(0, os.path.join(REPO, "tools"))
-    import step_stamps
-    step_stamps.build(stamped=("craft_sim", "craft_tile"))
+    import diag_build
+    diag_build.build(stamped=("craft_sim", "craft_tile"))
     sys.exit(0)
 import torch
 from psketch_amd import _native
