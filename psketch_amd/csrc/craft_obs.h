@@ -270,26 +270,18 @@ __device__ __forceinline__ void scatter_env_compact(const SimView& v, const uint
         }
 #pragma unroll
       for (int c = 0; c < W2; ++c) rec[c] = kk[c] ? (1u << kk[c]) : 0u;
-      // the tail: inventory bytes [0, K), dir one-hot [K, K + 4), then zeros
+      // the tail: inventory bytes [0, K) (tail word t is inventory word t, its bytes past K
+      // cleared), the dir one-hot at byte K + dir, then zeros (K <= 32: at most 10 words)
       const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);
-      uint32_t w[8];
+      const int TW = compact_tail_words(K), db = K + dir;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) w[q] = ivw[q];
-      const int TW = compact_tail_words(K);
-#pragma unroll 1
-      for (int t = 0; t < TW; ++t) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int i = 4 * t + b;
-          uint32_t wi = 0;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) wi = (q == (i >> 2)) ? w[q] : wi;
-          const uint32_t inv_b = (wi >> (8 * (i & 3))) & 0xffu;
-          const uint32_t val = i < K ? inv_b : (i - K == dir ? 1u : 0u);   // i - K == 4: the 0
-          o |= val << (8 * b);
+      for (int t = 0; t < (CRAFT_MAX_KINDS + 5 + 3) / 4; ++t) {
+        if (t < TW) {
+          const int nb = min(max(K - 4 * t, 0), 4);                   // inventory bytes in word t
+          uint32_t o = t < 8 ? (ivw[t] & (nb == 4 ? ~0u : (1u << (8 * nb)) - 1u)) : 0u;
+          o |= ((db >> 2) == t) ? (1u << (8 * (db & 3))) : 0u;
+          rec[2 * W2 + t] = o;
         }
-        rec[2 * W2 + t] = o;
       }
     } else {
       const int cx = cxa + unit - 1;
@@ -354,10 +346,12 @@ __device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint
   const int G = F >> 2;                        // groups per row
   const int total = nE * F;
   const int nv = total / PER;
-  const float invG = 1.0f / (float)G;
   uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
   constexpr int U = 4;
+  // the lane's group gg = sidx * GPS + j as (row e, group q), advanced by NTHR * GPS groups per
+  // store slot instead of divided each time
+  int ge = (tid * GPS) / G, gq = tid * GPS - ge * G;
   for (int base = tid; base < nv; base += U * NTHR) {
     obs_vec o[U];
 #pragma unroll
@@ -365,17 +359,16 @@ __device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint
       const int sidx = base + u * NTHR;
       if (sidx < nv) {
         uint32_t b[GPS];
+        int e = ge, q = gq;
 #pragma unroll
         for (int j = 0; j < GPS; ++j) {
-          const int gg = sidx * GPS + j;
-          int e = (int)((float)gg * invG);       // then corrected: exact for any tile
-          e -= (e * G > gg) ? 1 : 0;
-          e += ((e + 1) * G <= gg) ? 1 : 0;
-          const int q = gg - e * G;
           b[j] = group_bytes(s_rec + e * RS, s_desc[q]);
+          if (++q == G) { q = 0; ++e; }
         }
         o[u] = pack_bytes<FMT>(b);
       }
+      gq += NTHR * GPS;                          // the next store slot of this lane
+      while (gq >= G) { gq -= G; ++ge; }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {

@@ -316,6 +316,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   s->view.cpt = craft::compact_ok(cfg->window_width, cfg->n_kinds, cfg->n_features) &&
                 !(cpt_env && atoi(cpt_env) == 0) ? 1 : 0;
   s->tile = default_tile(cfg->window_width, s->view.cpt != 0);
+  const char* prio_env = getenv("CRAFT_T2_PRIO");
+  s->view.t2_prio = prio_env ? atoi(prio_env) : 0;
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
