@@ -50,6 +50,12 @@ struct SimView {
   int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
   int32_t cpt;                // 1: the tile kernel stages compact records (craft_obs.h), 5x5 / 7x7 windows
   int32_t t2_prio;            // tick2 kernel wave priorities (CRAFT_T2_PRIO, an A/B knob; 0 = none)
+  // The teacher's BFS answers on every pool row's pristine grid (craft_teach.h teach_table):
+  // ttab[((row * tt_slots + slot) * 4 + dir) * C + cell], slot = the target kind's slot
+  // (tt_slot: 4 bits per kind id, 0xf = none); null when the table is off (too large)
+  const uint16_t* ttab;
+  int32_t tt_slots;
+  uint64_t tt_slot[2];
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
   // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16.  Kernels copy the table to LDS.

@@ -27,6 +27,8 @@ hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const Ti
                              hipStream_t st);
 hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
 size_t tick2_lds_bytes(int tl, int GS, int F);
+hipError_t launch_teach_table(int nw, const SimView& v, int32_t first, int32_t count, const int32_t* kinds,
+                              hipStream_t st);
 
 namespace {
 
@@ -146,6 +148,8 @@ struct craft_sim {
   int32_t* d_task_sub = nullptr;
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
+  uint16_t* d_ttab = nullptr;       // the teacher table (craft_teach.h), or null
+  int32_t tt_kinds[16] = {};        // its slots' target kinds
   SimView view{};
   int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
   int tile_knob = 0;                // craft_sim_tune's tile_envs (0 = each kernel's default)
@@ -365,6 +369,32 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   s->sync_bytes = (16 + 4 * (size_t)((n_envs + 15) / 16) + 15) & ~size_t(15);   // queue + tile_done
   ALLOC(s->d_sync, s->sync_bytes);
   ALLOC(s->d_sync_graph, s->sync_bytes);      // craft_rollout launches captured into a graph
+  // The teacher table: one slot per kind some go[] or get[] task targets (teach_env's BFS kinds
+  // and the rollout summary's), 4 directions x C start cells per pool row, u16 entries.  Off
+  // (null: every query searches) past 1 GiB, past 2^21 rows (s_tinfo packs the row in 21 bits)
+  // or with CRAFT_TEACH_TABLE=0 (the A/B and parity switch).
+  {
+    int nslot = 0;
+    uint64_t smap[2] = {~0ull, ~0ull};
+    for (int t = 0; t < cfg->n_tasks; ++t) {
+      const craft_task_t& tk = cfg->task[t];
+      const int k = tk.arg_kind;
+      if ((tk.goal != CRAFT_GOAL_GO && tk.goal != CRAFT_GOAL_GET) || k <= 0 || k >= 32) continue;
+      if (((smap[k >> 4] >> (4 * (k & 15))) & 0xfull) != 0xfull) continue;      // has a slot
+      if (nslot >= 15) continue;                                                    // no room: BFS
+      smap[k >> 4] &= ~(0xfull << (4 * (k & 15)));
+      smap[k >> 4] |= (uint64_t)nslot << (4 * (k & 15));
+      s->tt_kinds[nslot++] = k;
+    }
+    const char* tt_env = getenv("CRAFT_TEACH_TABLE");
+    const size_t tt_bytes = (size_t)pool_capacity * nslot * 4 * C * sizeof(uint16_t);
+    if (nslot > 0 && pool_capacity < (1 << 21) && tt_bytes <= ((size_t)1 << 30) && !(tt_env && atoi(tt_env) == 0)) {
+      ALLOC(s->d_ttab, tt_bytes);
+      s->view.tt_slots = nslot;
+      s->view.tt_slot[0] = smap[0];
+      s->view.tt_slot[1] = smap[1];
+    }
+  }
 #undef ALLOC
   if ((e = hipMemcpy(s->d_task, task_tab.data(), sizeof(uint16_t) * task_tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "task table");
@@ -384,6 +414,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.task_sub = s->d_task_sub;
   v.stats_part = s->d_stats;
   v.err = s->d_err;
+  v.ttab = s->d_ttab;
   v.n_envs = n_envs;
   v.env_base = env_id_base;
   v.pool_count = 0;
@@ -479,6 +510,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_err);
   (void)hipFree(s->d_sync);
   (void)hipFree(s->d_sync_graph);
+  (void)hipFree(s->d_ttab);
   delete s;
   return CRAFT_OK;
 }
@@ -551,6 +583,10 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
   if (count) {
     HIP_TRY(s, hipMemcpy(s->d_pool + (size_t)first * CS, staged.data(), staged.size(), hipMemcpyHostToDevice));
     HIP_TRY(s, hipMemcpy(s->d_pool_conn + first, conn.data(), count, hipMemcpyHostToDevice));
+    // the rows' teacher-table entries (synchronous, like the load itself)
+    HIP_TRY(s, craft::launch_teach_table(craft::teach_words(s->view.W, s->view.H), s->view, first, count,
+                                         s->tt_kinds, nullptr));
+    HIP_TRY(s, hipStreamSynchronize(nullptr));
   }
   if (first + count > s->pool_count) s->pool_count = first + count;
   s->view.pool_count = s->pool_count;
@@ -589,6 +625,9 @@ int craft_pool_generate(craft_sim_t* s, uint64_t seed, int64_t scenario_id0, int
   HIP_TRY(s, hipSetDevice(s->device));
   hipError_t e = craft::launch_scenarios(s->view, a, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_pool_generate launch");
+  e = craft::launch_teach_table(craft::teach_words(s->view.W, s->view.H), s->view, first, count, s->tt_kinds,
+                                reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(s, e, "craft_pool_generate teacher table");
   if (first + count > s->pool_count) s->pool_count = first + count;
   s->view.pool_count = s->pool_count;
   return CRAFT_OK;
@@ -665,7 +704,8 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
     const int tile = craft::kMaxTileEnvs;
     const size_t lds = (size_t)craft::tile_lds_layout(tile, s->view.GS, s->view.F, s->view.cpt != 0,
                                                       s->cfg.window_width, s->view.K).bytes + tile * 4 +
-                       CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16;   // + task | frozen words, task_sub, D sync
+                       CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16 + tile * 4;
+    // + task | frozen words, task_sub, D sync and the deferred-BFS controls, the deferred list
     e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, s->view, a, lds, st);
   }
   if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");

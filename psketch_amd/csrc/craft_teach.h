@@ -504,6 +504,27 @@ __device__ __forceinline__ void band_bits(const uint32_t* row32, int nq, int C, 
   tgt = band(tgt, vb);
 }
 
+// ---- the teacher table: find_closest_resources answered ahead of time on pristine grids ----------
+// Every env of a scenario starts from the same pool row, and until it clears a cell (grab,
+// bridge, axe) its grid IS that row, so the BFS result depends only on (row, target kind, dir,
+// cell).  teach_table_kernel (craft_teacher.hip) evaluates bfs_closest for every such key when
+// rows are loaded; a query on an env whose cleared-cell mask is empty reads its answer instead
+// of running the BFS (the same function, evaluated earlier: bit-identical by construction).
+// Entry: bit 15 set = computed; bit 14 = ok (false: the reference raises, base.py:31);
+// bits 10-12 = first action + 1; bits 0-9 = path length + 1 (-1: no target).
+__device__ __forceinline__ int tt_slot_of(const SimView& v, int kind) {
+  if (kind < 0 || kind >= 32) return -1;
+  const int s = (int)((v.tt_slot[kind >> 4] >> (4 * (kind & 15))) & 0xfu);
+  return s == 0xf ? -1 : s;
+}
+__device__ __forceinline__ uint16_t tt_encode(bool ok, int fa, int len) {
+  return (uint16_t)(0x8000u | (ok ? 0x4000u : 0u) | ((uint32_t)(fa + 1) << 10) | (uint32_t)(len + 1));
+}
+// The table row block of scenario `scen` (null when there is no table).
+__device__ __forceinline__ const uint16_t* tt_row(const SimView& v, int scen) {
+  return v.ttab ? v.ttab + (size_t)scen * v.tt_slots * 4 * v.C : nullptr;
+}
+
 // DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for one env, LANES
 // lanes of a quad-aligned group (lane ql of the group).  Its current grid is row32
 // (kind ids, x-major, as 32-bit words; NW*8 words at most) minus the cells set in m
@@ -512,12 +533,28 @@ __device__ __forceinline__ void band_bits(const uint32_t* row32, int nq, int C, 
 // (pool_conn); task_tab / task_sub are the handle's task tables
 // (v.task_tab / v.task_sub, or copies in LDS).  Returns the action, or -2 where the reference
 // raises (err_out = CRAFT_ETEACHER).  With want_len, len_out receives
-// len(find_closest_resources(task.arg)) (-1: no target, -2: the reference raises).
-template <int NW, int LANES>
+// len(find_closest_resources(task.arg)) (-1: no target, -2: the reference raises).  ttab: the
+// teacher-table block of the env's scenario when its grid is pristine (no cell cleared), else
+// null: a target kind with a table slot is then read off the table instead of searched.
+// The action for a go[X] leaf from find_closest_resources' answer (demonstration.py:23-30).
+__device__ __forceinline__ int go_leaf_action(bool ok, int fa, int len, int& err) {
+  if (!ok) err = CRAFT_ETEACHER;                    // base.py:31 len(None)
+  else if (len < 0) return CRAFT_STOP;              // demonstration.py:25-26
+  else if (len == 0) err = CRAFT_ETEACHER;          // [][0]
+  else return fa;
+  return -2;
+}
+
+// DEFER (the fused kernels; no want_len): no BFS here at all.  A go[X] leaf the table cannot
+// answer returns kTeachDeferred with *defer = X, for a later dense pass (teach_deferred).
+constexpr int kTeachDeferred = -3;
+
+template <int NW, int LANES, bool DEFER = false>
 __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_tab, const int32_t* task_sub,
                                          const uint32_t* row32, const uint32_t (&m)[8],
                                          const uint8_t* iv, const Agent& s, int task, int ql,
-                                         bool want_len, int& len_out, int& err_out, bool conn) {
+                                         bool want_len, int& len_out, int& err_out, bool conn,
+                                         const uint16_t* ttab = nullptr, int* defer = nullptr) {
   const int H = v.H, C = v.C;
   auto kind_at = [&](int c) -> int {
     const uint32_t w = row32[c >> 2];
@@ -537,6 +574,15 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
   const Bits<NW> valid = brange<NW>(0, C - 2 * H);      // the band of columns 1 .. W-2
   const int nq = (C + 3) >> 2;
   auto closest = [&](int kind, int& fa, int& len, bool want_action) -> bool {
+    const int slot = ttab ? tt_slot_of(v, kind) : -1;
+    if (slot >= 0) {                                      // group-uniform: one load per lane
+      const uint32_t e = ttab[(slot * 4 + s.dir) * C + s.x * H + s.y];
+      if (e & 0x8000u) {
+        fa = want_action ? (int)((e >> 10) & 7u) - 1 : -1;
+        len = (int)(e & 0x3ffu) - 1;
+        return (e & 0x4000u) != 0;
+      }
+    }
     Bits<NW> occ, tgt;
     band_bits<NW, LANES>(row32, nq, C, H, m, (uint32_t)kind, ql, occ, tgt);
 #ifdef CRAFT_ABL_NOBFS
@@ -571,13 +617,21 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
       if (goal == CRAFT_GOAL_USE) {
         action = CRAFT_USE;
       } else if (goal == CRAFT_GOAL_GO) {
-        int fa = -1, len = -1;
-        leaf_ok = closest(arg, fa, len, true);
-        leaf_kind = arg; leaf_fa = fa; leaf_len = len;
-        if (!leaf_ok) err = CRAFT_ETEACHER;
-        else if (len < 0) action = CRAFT_STOP;                           // demonstration.py:25-26
-        else if (len == 0) err = CRAFT_ETEACHER;                         // [][0]
-        else action = fa;
+        if constexpr (DEFER) {
+          const int slot = ttab ? tt_slot_of(v, arg) : -1;
+          const uint32_t e = slot >= 0 ? ttab[(slot * 4 + s.dir) * C + s.x * H + s.y] : 0u;
+          if (!(e & 0x8000u)) {
+            *defer = arg;                                                // a BFS, done densely later
+            err_out = 0;
+            return kTeachDeferred;
+          }
+          action = go_leaf_action((e & 0x4000u) != 0, (int)((e >> 10) & 7u) - 1, (int)(e & 0x3ffu) - 1, err);
+        } else {
+          int fa = -1, len = -1;
+          leaf_ok = closest(arg, fa, len, true);
+          leaf_kind = arg; leaf_fa = fa; leaf_len = len;
+          action = go_leaf_action(leaf_ok, fa, len, err);
+        }
       } else {
         err = CRAFT_ETEACHER;                                            // demonstration.py:18
       }
@@ -585,7 +639,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
   }
   if (err) action = -2;                // where the reference raises
   err_out = err;
-  if (want_len) {
+  if (!DEFER && want_len) {
     const int arg = (task_tab[task] >> 4) & 0xff;
     int fa = leaf_fa, len = leaf_len;
     bool ok = leaf_ok;
@@ -596,6 +650,38 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
     len_out = ok ? len : -2;
   }
   return action;
+}
+
+
+// The deferred BFS queries of a workgroup, densely: work[k] = env index | target kind << 8 for
+// k < n, answered by the workgroup's teacher lane groups in order (group g takes k = g; every env
+// defers at most one query and there is one group per env, so n <= G), so a wave spends its BFS
+// instructions on envs that need one instead of on the few of its own.  grid / agent / info as the fused kernels keep them in LDS (info: task |
+// frozen << 8 | connected << 9); label: the label row of the workgroup's first env.
+template <int NW, int LANES>
+__device__ __forceinline__ void teach_deferred(const SimView& v, const uint32_t* work, int n, int g, int G, int ql,
+                                               const uint8_t* s_grid, int GS, const uint32_t* s_agent,
+                                               const uint32_t* s_info, int32_t* label, int64_t env0) {
+  const int H = v.H, C = v.C, nq = (C + 3) >> 2;
+  const Bits<NW> valid = brange<NW>(0, C - 2 * H);
+  const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (g < n) {
+    const uint32_t wk = work[g];
+    const int e = wk & 0xff, kind = (wk >> 8) & 0xff;
+    const uint32_t ag = s_agent[e], ti = s_info[e];
+    const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+    Bits<NW> occ, tgt;
+    band_bits<NW, LANES>(reinterpret_cast<const uint32_t*>(s_grid + e * GS), nq, C, H, m0, (uint32_t)kind, ql,
+                         occ, tgt);
+    int fa = -1, len = -1, err = 0;
+    const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, H, x * H + y - H, dir, ql, fa, len, true,
+                                           ((ti >> 9) & 1u) != 0);
+    const int action = go_leaf_action(ok, fa, len, err);
+    if (ql == 0) {
+      if (err) latch_error(v.err, err, env0 + e);
+      label[e] = action;
+    }
+  }
 }
 
 }  // namespace craft

@@ -82,9 +82,11 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   }
   const uint8_t* iv = reinterpret_cast<const uint8_t*>(v.inv + 2 * slot);
   const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
+  const bool pristine = (m[0] | m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7]) == 0u;
   int len = -1, err = 0;
   const int action = teach_env<NW, LANES>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
-                                          len, err, v.pool_conn[s.scen] != 0);
+                                          len, err, v.pool_conn[s.scen] != 0,
+                                          pristine ? tt_row(v, s.scen) : nullptr);
   if (lead) {
     if (err) latch_error(v.err, err, slot);
     a.act_out[i] = action;
@@ -145,14 +147,22 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
       d = -2;
     } else {
       const int C = v.C, nq = (C + 3) >> 2;
-      const Bits<NW> valid = brange<NW>(0, C - 2 * v.H);    // the band of columns 1 .. W-2
-      const uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
-      Bits<NW> occ, tgt;
-      band_bits<NW, LANES>(row32, nq, C, v.H, m, (tt >> 4) & 0xffu, ql, occ, tgt);
+      const int kind = (tt >> 4) & 0xffu, slot = v.ttab ? tt_slot_of(v, kind) : -1;
+      const uint32_t e = slot >= 0 ? tt_row(v, s.scen)[(slot * 4 + s.dir) * C + s.x * v.H + s.y] : 0u;
       int fa = -1, len = -1;
-      const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, v.H, s.x * v.H + s.y - v.H, s.dir, ql, fa, len,
-                                             false, v.pool_conn[s.scen] != 0);
+      bool ok;
+      if (e & 0x8000u) {                 // the initial grid is the pool row: the teacher table's
+        len = (int)(e & 0x3ffu) - 1;     // answer (craft_teach.h)
+        ok = (e & 0x4000u) != 0;
+      } else {
+        const Bits<NW> valid = brange<NW>(0, C - 2 * v.H);  // the band of columns 1 .. W-2
+        const uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
+        Bits<NW> occ, tgt;
+        band_bits<NW, LANES>(row32, nq, C, v.H, m, kind, ql, occ, tgt);
+        ok = bfs_closest<NW, LANES>(occ, tgt, valid, v.H, s.x * v.H + s.y - v.H, s.dir, ql, fa, len, false,
+                                    v.pool_conn[s.scen] != 0);
+      }
       // !ok: a target the BFS cannot reach.  The reference raises the same TypeError, len(None),
       // whether no target exists or none (or a later one, base.py:31) is reachable, so both
       // report through flags[1] below and nothing latches
@@ -168,6 +178,61 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
     if (succ < 0) a.flags[0] = 1;
     if ((d == -1 || d == -2) && is_get && succ == 0) a.flags[1] = 1;
   }
+}
+
+// ---- the teacher table (craft_teach.h): bfs_closest on the pristine grid of pool rows
+// [first, first + count) for every target-kind slot, direction and free interior start cell,
+// LANES lanes per key.  Occupied and border cells get 0 (never read: an agent stands on a free
+// interior cell, and a pristine grid is the row itself). ------------------------------------------
+struct TableArgs {
+  int32_t first, count;
+  int32_t kinds[16];         // slot -> target kind
+};
+
+template <int NW, int LANES>
+__global__ __launch_bounds__(256) void teach_table_kernel(SimView v, TableArgs a) {
+  const int C = v.C, H = v.H, S = v.tt_slots;
+  const int64_t per_row = (int64_t)S * 4 * C;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
+  const int ql = (int)(threadIdx.x % LANES);
+  if (i >= (int64_t)a.count * per_row) return;          // lane-group-uniform
+  const int r = (int)(i / per_row);
+  const int k = (int)(i - (int64_t)r * per_row);
+  const int slot = k / (4 * C), dir = (k / C) & 3, cell = k % C;
+  const int row = a.first + r;
+  const uint8_t* g = v.pool + (size_t)row * v.CS;
+  const int x = cell / H, y = cell - x * H;
+  uint16_t e = 0;
+  if (x >= 1 && x <= v.W - 2 && y >= 1 && y <= H - 2 && g[cell] == 0) {
+    const uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const Bits<NW> valid = brange<NW>(0, C - 2 * H);
+    Bits<NW> occ, tgt;
+    band_bits<NW, LANES>(reinterpret_cast<const uint32_t*>(g), (C + 3) >> 2, C, H, m, (uint32_t)a.kinds[slot], ql,
+                         occ, tgt);
+    int fa = -1, len = -1;
+    const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, H, cell - H, dir, ql, fa, len, true, v.pool_conn[row] != 0);
+    e = tt_encode(ok, fa, len);
+  }
+  if (ql == 0) const_cast<uint16_t*>(v.ttab)[(size_t)row * per_row + k] = e;
+}
+
+hipError_t launch_teach_table(int nw, const SimView& v, int32_t first, int32_t count, const int32_t* kinds,
+                              hipStream_t st) {
+  if (!v.ttab || count <= 0 || v.tt_slots <= 0) return hipSuccess;
+  TableArgs a{};
+  a.first = first;
+  a.count = count;
+  for (int s = 0; s < v.tt_slots && s < 16; ++s) a.kinds[s] = kinds[s];
+  constexpr int LANES = 2;
+  const int64_t items = (int64_t)count * v.tt_slots * 4 * v.C;
+  const unsigned blocks = (unsigned)((LANES * items + 255) / 256);
+#define CRAFT_TT(NWV) hipLaunchKernelGGL((teach_table_kernel<NWV, LANES>), dim3(blocks), dim3(256), 0, st, v, a)
+  if (nw <= 2) CRAFT_TT(2);
+  else if (nw <= 4) CRAFT_TT(4);
+  else if (nw <= 5) CRAFT_TT(5);
+  else CRAFT_TT(8);
+#undef CRAFT_TT
+  return hipGetLastError();
 }
 
 hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, const int8_t* success,

@@ -38,7 +38,7 @@ constexpr int kTick2Tile = 64;          // envs per tile (one lane each in A + C
 // teacher info words [J*64] | task table [64] u16 | task_sub [64][4] | recipe words [16][3] |
 // observation rows [TW waves][up16(64/TW*F)]
 struct Tick2Lds {
-  int inv, agent, tinfo, task, tsub, rc, obs, bytes;
+  int inv, agent, tinfo, task, tsub, rc, work, obs, bytes;
 };
 __host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -50,7 +50,8 @@ __host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F) {
   l.task = l.tinfo + n * 4;
   l.tsub = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.rc = l.tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4;
-  l.obs = up16(l.rc + CRAFT_MAX_RECIPES * 12);
+  l.work = up16(l.rc + CRAFT_MAX_RECIPES * 12);   // deferred BFS list [n] + {count, arrivals}
+  l.obs = up16(l.work + n * 4 + 8);
   l.bytes = l.obs + TW * up16(kTick2Tile / TW * F);
   return l;
 }
@@ -73,13 +74,24 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
+  uint32_t* s_work = reinterpret_cast<uint32_t*>(smem + lay.work);       // deferred BFS queries
+  uint32_t* s_wctl = s_work + J * kTick2Tile;                           // {count, teacher arrivals}
   const int obs_w = (kTick2Sub * F + 15) & ~15;
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t envw = (int64_t)blockIdx.x * (J * kTick2Tile);          // this workgroup's first env
   // CRAFT_STAMPS builds (tools/tick2_stamps.py): 0 start, 1 wave 0's loads landed, 2 wave 0's C
   // done, 3 past the barrier, 4 wave 0's first store issued, 5 the last tick wave done issuing
-  // stores, 6 the last teacher wave done, 7 the XCC
+  // stores, 6 the last teacher wave done, 7 the XCC.  With CRAFT_STAMPS_C, wave 0's A + C in
+  // detail instead: 1 the state word landed, 2 the pool row in LDS, 3 the pre-step tests and
+  // cleared cells applied, 4 the transition done, 5 its global stores issued, 6 C done.
+#ifdef CRAFT_STAMPS_C
+#define T2S(k, kc) do { if ((kc) >= 0) STAMP((kc) < 0 ? 0 : (kc)); } while (0)
+#define T2SM(k) do {} while (0)
+#else
+#define T2S(k, kc) do { if ((k) >= 0) STAMP((k) < 0 ? 0 : (k)); } while (0)
+#define T2SM(k) STAMP_MAX(k)
+#endif
   STAMP(0);
   const bool want_obs = a.obs != nullptr;
   auto tile_envs = [&](int j) { return (int)max((int64_t)0, min((int64_t)kTick2Tile, a.n - envw - j * kTick2Tile)); };
@@ -121,6 +133,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q) sw[q] = TL > 0 ? v.task_sub[lane + 64 * q] : 0;
     if (lane < v.n_tasks) s_task[lane] = (uint16_t)tw;
     if (lane < CRAFT_MAX_RECIPES * 3) s_rc[lane] = rw;
+    if (TL > 0 && j == 0 && lane < 2) s_wctl[lane] = 0u;                  // (before the barrier)
     if (TL > 0) {
 #pragma unroll
       for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q)
@@ -139,6 +152,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
         live = false;
       }
     }
+    if (j == 0) T2S(-1, 1);
     uint8_t* g = s_grid + le * GS;
     uint32_t conn = 0;
     if (TL > 0 && live) conn = v.pool_conn[s.scen];
@@ -159,7 +173,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    STAMP(1);
+    if (j == 0) T2S(1, 2);
 
     uint32_t* ivw = reinterpret_cast<uint32_t*>(s_inv + le * kInvStride);
     uint8_t* iv = s_inv + le * kInvStride;
@@ -201,6 +215,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
           }
         }
       }
+      if (j == 0) T2S(-1, 3);
       if (restart) {                                                     // CraftScenario.init, craft.py:268-273
         s.x = init_word & 0xff; s.y = (init_word >> 8) & 0xff; s.dir = (init_word >> 16) & 3;
         s.timer = v.maxT;
@@ -219,6 +234,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
           code = transition_code(ox, oy, s, inv_changed);
         }
       }
+      if (j == 0) T2S(-1, 4);
       v.state[slot] = pack_state(s);
       if (inv_changed) {
         v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
@@ -233,9 +249,16 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       if (a.reward) a.reward[slot] = (counted && d && succ == 1) ? 1.0f : 0.0f;
       if (a.rec) a.rec[slot] = counted ? act : -1;                       // action_seqs, imitation.py:59-61
     }
+    if (j == 0) T2S(-1, 5);
     if (a.code && lane < nE) a.code[slot] = (int8_t)code;
     s_agent[le] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
-    if (TL > 0) s_tinfo[le] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9);
+    // the teacher's inputs: task | frozen << 8 | scenario connected << 9 | grid pristine (no cell
+    // cleared: the teacher table answers, craft_teach.h) << 10 | scenario << 11 (< 2^21 when the
+    // table is on)
+    if (TL > 0)
+      s_tinfo[le] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9) |
+                      ((m[0] | m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7]) == 0u ? 1u << 10 : 0u) |
+                      ((uint32_t)s.scen << 11);
     // episode statistics: the partial-sum row of this 64-env tile (uncontended)
     const uint64_t bs = __ballot(live && counted && d && succ == 1);
     const uint64_t be = __ballot(live && counted && d);
@@ -249,7 +272,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       atomicAdd(r + 2, (unsigned long long)__popcll(bt));
       if (a.any_live && bl) *a.any_live = 1;                             // idempotent plain store
     }
-    STAMP(2);
+    if (j == 0) T2S(2, 6);
   } else if (want_obs && wave < kTick2Waves) {
     // waves J..3: zero the observation rows of every tick wave
     uint4* z = reinterpret_cast<uint4*>(smem + lay.obs);
@@ -258,7 +281,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   }
   if (TL == 0 && !want_obs) return;                                      // no barrier follows
   __syncthreads();
-  STAMP(3);
+  T2S(3, -1);
 
   if (wave < kTick2Waves) {
     if (!want_obs) return;
@@ -275,7 +298,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (j == 0) STAMP(4);
+      if (j == 0) T2S(4, -1);
       switch (v.obs_fmt) {
         case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
         case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
@@ -285,7 +308,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    STAMP_MAX(5);
+    T2SM(5);
 #ifdef CRAFT_STAMPS
     if (tid == 0 && v.stamps) {
       uint32_t xcc;
@@ -317,16 +340,32 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
         Agent s{};
         s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int len = -1, err = 0;
-        action = teach_env<NW, TL>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + le * GS), m0,
+        int len = -1, err = 0, defer = -1;
+        // the hint walk, and the teacher table for a pristine grid; a BFS left over is deferred
+        action = teach_env<NW, TL, true>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + le * GS), m0,
                                    s_inv + le * kInvStride, s, s.task, ql, false, len, err,
-                                   ((ti >> 9) & 1u) != 0);
+                                   ((ti >> 9) & 1u) != 0, ((ti >> 10) & 1u) ? tt_row(v, (int)(ti >> 11)) : nullptr,
+                                   &defer);
         if (err && ql == 0) latch_error(v.err, err, i);
+        if (action == kTeachDeferred && ql == 0)
+          s_work[__hip_atomic_fetch_add(&s_wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
+              (uint32_t)le | ((uint32_t)defer << 8);
       }
-      if (ql == 0) a.label[i] = action;
+      if (ql == 0 && action != kTeachDeferred) a.label[i] = action;
     }
-    STAMP_MAX(6);
+    // every teacher wave has listed its deferred queries; then all of them run the BFS densely
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((tid & 63) == 0) __hip_atomic_fetch_add(&s_wctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&s_wctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)(J * TL))
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t nw = __hip_atomic_load(&s_wctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    teach_deferred<NW, TL>(v, s_work, (int)nw, u / TL, J * kTick2Tile, ql, s_grid, GS, s_agent, s_tinfo,
+                           a.label + envw, envw);
+    T2SM(6);
   }
 }
+#undef T2S
+#undef T2SM
 
 }  // namespace craft

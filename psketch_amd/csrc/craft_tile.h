@@ -49,6 +49,8 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
   uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.bytes);   // TL > 0: [TILE] task | frozen << 8
   int32_t* s_tsub = reinterpret_cast<int32_t*>(s_tinfo + TILE);           // TL > 0: task_sub copy
   uint32_t* s_dsync = reinterpret_cast<uint32_t*>(s_tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS);   // TL > 0
+  uint32_t* s_wctl = s_dsync + 1;           // TL > 0: {deferred BFS count, teacher arrivals} (craft_teach.h)
+  uint32_t* s_work = s_dsync + 4;           // TL > 0: the deferred BFS queries [TILE]
 
   const int tid = threadIdx.x;
   const int64_t env0 = (int64_t)blockIdx.x * TILE;
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
 #pragma unroll
       for (int q = 0; q < QS; ++q)
         if (tid + q * TILE < v.n_tasks * CRAFT_MAX_SUBTASKS) s_tsub[tid + q * TILE] = sw[q];
-      if (tid == 0) *s_dsync = 0u;
+      if (tid == 0) { *s_dsync = 0u; s_wctl[0] = 0u; s_wctl[1] = 0u; }
     }
     if (live) {
       if (MODE == MODE_RESET) {
@@ -282,7 +284,13 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
     }
     if ((MODE == MODE_TICK || MODE == MODE_TRANSITION) && a.code && tid < nE) a.code[env0 + tid] = (int8_t)code;
     s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
-    if (TL > 0) s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9);
+    // the teacher's inputs: task | frozen << 8 | scenario connected << 9 | grid pristine (no cell
+    // cleared: the teacher table answers, craft_teach.h) << 10 | scenario << 11 (< 2^21 when the
+    // table is on)
+    if (TL > 0)
+      s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9) |
+                      ((m[0] | m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7]) == 0u ? 1u << 10 : 0u) |
+                      ((uint32_t)s.scen << 11);
     if (MODE == MODE_TICK) {
       // episode statistics: one partial-sum row per workgroup (uncontended)
       const uint64_t bs = __ballot(live && counted && d && succ == 1);
@@ -353,14 +361,28 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
         Agent s{};
         s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int len = -1, err = 0;
-        action = teach_env<NW, TL>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS),
+        int len = -1, err = 0, defer = -1;
+        // the hint walk, and the teacher table for a pristine grid; a BFS left over is deferred
+        action = teach_env<NW, TL, true>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS),
                                    m0, s_inv + e * kInvStride, s, s.task, ql, false, len, err,
-                                   ((ti >> 9) & 1u) != 0);
+                                   ((ti >> 9) & 1u) != 0, ((ti >> 10) & 1u) ? tt_row(v, (int)(ti >> 11)) : nullptr,
+                                   &defer);
         if (err && ql == 0) latch_error(v.err, err, i);
+        if (action == kTeachDeferred && ql == 0)
+          s_work[__hip_atomic_fetch_add(&s_wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
+              (uint32_t)e | ((uint32_t)defer << 8);
       }
-      if (ql == 0) a.label[i] = action;
+      if (ql == 0 && action != kTeachDeferred) a.label[i] = action;
     }
+    // every teacher wave has listed its deferred queries; then all of them run the BFS densely
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((tid & 63) == 0) __hip_atomic_fetch_add(&s_wctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(&s_wctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)(TILE * TL / 64))
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t nw = __hip_atomic_load(&s_wctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    teach_deferred<NW, TL>(v, s_work, (int)nw, u / TL, TILE, ql, s_grid, v.GS, s_agent, s_tinfo, a.label + env0,
+                           env0);
     STAMP_END();
     return;
   }

@@ -2,7 +2,7 @@
 from the product's objects except the named translation units, which are compiled again with
 -DCRAFT_STAMPS (s_memrealtime phase stamps, craft_device.h) and any extra defines.
 
-    python tools/diag_build.py craft_sim craft_tile [-DNAME ...]"""
+    python tools/diag_build.py craft_sim craft_tile [-DNAME ...] [--out libname.so]"""
 import os
 import subprocess
 import sys
@@ -14,10 +14,10 @@ import __graft_entry__ as ge  # noqa: E402
 DIAG = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_diag.so")
 
 
-def build(stamped=("craft_sim", "craft_tile"), defines=()):
+def build(stamped=("craft_sim", "craft_tile"), defines=(), out=DIAG):
     ge.build()
     obj = os.path.join(REPO, "psketch_amd", "lib", "obj")
-    dobj = os.path.join(REPO, "psketch_amd", "lib", "obj_diag")
+    dobj = os.path.join(REPO, "psketch_amd", "lib", "obj_diag" + "".join("_" + d[2:].lower() for d in defines))
     os.makedirs(dobj, exist_ok=True)
     objs = []
     for src in ge.SOURCES:
@@ -29,10 +29,16 @@ def build(stamped=("craft_sim", "craft_tile"), defines=()):
         else:
             o = os.path.join(obj, base + ".o")
         objs.append(o)
-    subprocess.check_call([ge.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", DIAG] + objs)
-    return DIAG
+    subprocess.check_call([ge.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs)
+    return out
 
 
 if __name__ == "__main__":
-    names = [a for a in sys.argv[1:] if not a.startswith("-D")]
-    build(tuple(names) or ("craft_sim", "craft_tile"), [a for a in sys.argv[1:] if a.startswith("-D")])
+    args = sys.argv[1:]
+    out = DIAG
+    if "--out" in args:                  # another diagnostic library name under psketch_amd/lib/
+        i = args.index("--out")
+        out = os.path.join(REPO, "psketch_amd", "lib", args[i + 1])
+        del args[i:i + 2]
+    names = [a for a in args if not a.startswith("-D")]
+    build(tuple(names) or ("craft_sim", "craft_tile"), [a for a in args if a.startswith("-D")], out)

@@ -24,10 +24,12 @@ def main():
     p.add_argument("--envs", type=int, default=65536)
     p.add_argument("--ring", type=int, nargs="+", default=[16, 1])
     p.add_argument("--ticks", type=int, default=30)
+    p.add_argument("--lib", default="libpsketch_craft_diag.so",
+                   help="diagnostic library; libpsketch_craft_diag_c.so (-DCRAFT_STAMPS_C): wave 0's A + C")
     args = p.parse_args()
     import torch
     from psketch_amd import _native
-    _native.LIB_PATH = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_diag.so")
+    _native.LIB_PATH = os.path.join(REPO, "psketch_amd", "lib", args.lib)
     from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
     lib = _native.lib()
     lib.craft_debug_set_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -42,6 +44,9 @@ def main():
     st = torch.zeros((wgs, 8), dtype=torch.int64, device="cuda")
     lib.craft_debug_set_stamps(sim._h, ctypes.c_void_p(st.data_ptr()))
     names = ["start", "loads", "C", "barrier", "first_store", "stores_issued", "teacher_done"]
+    if "diag_c" in args.lib:             # CRAFT_STAMPS_C: wave 0's A + C in detail
+        names = ["start", "state_landed", "row_in_lds", "pre_step_done", "transition_done", "stores_issued",
+                 "C_done"]
     for R in args.ring:
         ring = [sim.empty_obs() for _ in range(R)]
         lab = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -60,6 +65,9 @@ def main():
             v = r[:, :, i]
             out[nm] = {"p10": round(float(np.percentile(v, 10)), 2), "p50": round(float(np.median(v)), 2),
                        "p90": round(float(np.percentile(v, 90)), 2), "max": round(float(v.max(axis=1).mean()), 2)}
+        print(json.dumps(out) if "diag_c" in args.lib else "", end="\n" if "diag_c" in args.lib else "")
+        if "diag_c" in args.lib:
+            continue
         end = np.maximum(r[:, :, 5], r[:, :, 6])
         out["wg_end_max_mean"] = round(float(end.max(axis=1).mean()), 2)
         out["teacher_ends_wg_frac"] = round(float((r[:, :, 6] > r[:, :, 5]).mean()), 3)
