@@ -335,8 +335,62 @@ __device__ __forceinline__ obs_vec pack_bytes(const uint32_t* b) {
   }
 }
 
+// One feature value of a record pair (a0, a1) = rec[w0], rec[w0 + 1] by its descriptor byte c.
+__device__ __forceinline__ uint32_t desc_value(uint32_t a0, uint32_t a1, uint32_t c) {
+  return __builtin_amdgcn_ubfe((c & 1u) ? a1 : a0, (c >> 1) & 31u, (c & 64u) ? 8u : 1u);
+}
+
+// Phase E, fp32, compact records: every 16-byte store is one group of 4 features (F % 4 == 0,
+// rows 16-byte aligned).  Thread t owns group q = t (+ NTHR, ...) of every row: it decodes the
+// group's descriptor once, then per row reads its two record words and extracts 4 values (one
+// bit-field extract each), so a store costs ~15 instructions.  Consecutive lanes store
+// consecutive groups of one row (contiguous).  The G % NTHR groups left over go round flat.
+template <int NTHR = kThreads>
+__device__ __forceinline__ void stream_compact_f32(const uint32_t* s_rec, const uint64_t* s_desc, void* obs,
+                                                   int64_t env0, int F, int RS, int nE, int policy, int tid) {
+  const int G = F >> 2;
+  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * 4;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, nE * F * 4, 0x00020000);
+  auto put = [&](const obs_vec& o, int off) {
+    if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, off, 0, 2);          // nt
+    else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, off, 0, 16);    // sc1
+    else __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, off, 0, 0);
+  };
+  auto vals = [&](uint32_t a0, uint32_t a1, uint32_t hi) {
+    return obs_vec{__float_as_uint((float)desc_value(a0, a1, hi & 0xffu)),
+                   __float_as_uint((float)desc_value(a0, a1, (hi >> 8) & 0xffu)),
+                   __float_as_uint((float)desc_value(a0, a1, (hi >> 16) & 0xffu)),
+                   __float_as_uint((float)desc_value(a0, a1, hi >> 24))};
+  };
+  const int full = G / NTHR;
+  for (int r = 0; r < full; ++r) {
+    const int q = tid + r * NTHR;
+    const uint64_t d = s_desc[q];
+    const uint32_t hi = (uint32_t)(d >> 16);
+    const uint32_t* rp = s_rec + (uint32_t)(d & 0xffffu);
+    constexpr int U = 4;                               // stores in flight per lane
+    for (int e = 0; e < nE; e += U) {
+      obs_vec o[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (e + u < nE) o[u] = vals(rp[(e + u) * RS], rp[(e + u) * RS + 1], hi);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (e + u < nE) put(o[u], ((e + u) * G + q) * 16);
+    }
+  }
+  const int R = G - full * NTHR;                       // groups left over, every row
+  for (int f = tid; f < R * nE; f += NTHR) {
+    const int e = f / R, q = full * NTHR + (f - e * R);
+    const uint64_t d = s_desc[q];
+    const uint32_t* rp = s_rec + e * RS + (uint32_t)(d & 0xffffu);
+    put(vals(rp[0], rp[1], (uint32_t)(d >> 16)), (e * G + q) * 16);
+  }
+}
+
 // Phase E with compact records: the tile's rows as one flat stream of 16-byte stores (as
-// stream_obs), each store's 4 / 8 / 16 values read off the records by group descriptor.
+// stream_obs), each store's 4 / 8 / 16 values read off the records by group descriptor (the
+// bf16 / u8 formats, whose stores may straddle rows; fp32 takes stream_compact_f32).
 template <int FMT, int NTHR = kThreads>
 __device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint64_t* s_desc, void* obs,
                                                int64_t env0, int F, int RS, int nE, int policy, int tid) {

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
     switch (v.obs_fmt) {
       case CRAFT_OBS_BF16: stream_compact<CRAFT_OBS_BF16>(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
       case CRAFT_OBS_U8: stream_compact<CRAFT_OBS_U8>(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
-      default: stream_compact<CRAFT_OBS_F32>(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
+      default: stream_compact_f32(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
     }
     STAMP_END();
     return;
