@@ -21,24 +21,13 @@ struct TeachArgs {
   int32_t* len_out;
 };
 
-// DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30), LANES lanes per item:
-// 4 (quad-parallel BFS) gives each query the shortest dependent chain, which is what
-// bounds a small batch; 2 (a pair, one shift amount per lane) does about half the
-// instructions per query at nearly the same chain length, which is what bounds a large
-// one; 1 does the least work but the longest chain (launch_teacher picks by batch size).
-template <int NW, int LANES>
-__global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
-  // the task tables in LDS: the hint-tree walk reads them in a dependent chain
-  __shared__ uint16_t s_tab[CRAFT_MAX_TASKS];
-  __shared__ int32_t s_sub[CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS];
-  for (int t = threadIdx.x; t < v.n_tasks * CRAFT_MAX_SUBTASKS; t += blockDim.x) {
-    if (t < v.n_tasks) s_tab[t] = v.task_tab[t];
-    s_sub[t] = v.task_sub[t];
-  }
-  __syncthreads();
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
-  const int ql = (int)(threadIdx.x % LANES);
-  if (i >= a.n) return;                  // lane-group-uniform: a group never straddles two items
+// DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for item i, LANES lanes per
+// item.  Writes the item's outputs and returns -1, or with DEFER (no path lengths asked) returns
+// the target kind of a go[X] leaf the teacher table cannot answer, its BFS left to the
+// workgroup's dense pass (teacher_kernel).
+template <int NW, int LANES, bool DEFER>
+__device__ __forceinline__ int teach_item(const SimView& v, const TeachArgs& a, int64_t i, int ql,
+                                          const uint16_t* s_tab, const int32_t* s_sub) {
   const bool lead = ql == 0;             // the lane that writes the outputs and latches errors
   const int64_t slot = a.slots ? (int64_t)a.slots[i] : i;
   if (slot == -1) {                    // skipped item: the trainer's ref_action for a done env
@@ -46,7 +35,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
       a.act_out[i] = -1;
       if (a.len_out) a.len_out[i] = -1;
     }
-    return;
+    return -1;
   }
   if (slot < 0 || slot >= v.n_envs) {
     if (lead) {
@@ -54,7 +43,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
       a.act_out[i] = -2;
       if (a.len_out) a.len_out[i] = -2;
     }
-    return;
+    return -1;
   }
   const Agent s = unpack_state(v.state[slot]);
   if (s.frozen) {                      // done env: its label is -1 (imitation.py:50-51)
@@ -62,7 +51,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
       a.act_out[i] = -1;
       if (a.len_out) a.len_out[i] = -1;
     }
-    return;
+    return -1;
   }
   const int task = a.tasks ? a.tasks[i] : s.task;
   if (task < 0 || task >= v.n_tasks || s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 ||
@@ -72,7 +61,7 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
       a.act_out[i] = -2;
       if (a.len_out) a.len_out[i] = -2;
     }
-    return;
+    return -1;
   }
   uint32_t m[8];
   {
@@ -83,16 +72,73 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
   const uint8_t* iv = reinterpret_cast<const uint8_t*>(v.inv + 2 * slot);
   const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
   const bool pristine = (m[0] | m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7]) == 0u;
-  int len = -1, err = 0;
-  const int action = teach_env<NW, LANES>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
-                                          len, err, v.pool_conn[s.scen] != 0,
-                                          pristine ? tt_row(v, s.scen) : nullptr);
+  int len = -1, err = 0, defer = -1;
+  const int action = teach_env<NW, LANES, DEFER>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
+                                                 len, err, v.pool_conn[s.scen] != 0,
+                                                 pristine ? tt_row(v, s.scen) : nullptr, &defer);
+  if (DEFER && action == kTeachDeferred) return defer;
   if (lead) {
     if (err) latch_error(v.err, err, slot);
     a.act_out[i] = action;
     if (a.len_out) {
       if (len == -2) latch_error(v.err, CRAFT_ETEACHER, slot);
       a.len_out[i] = len;
+    }
+  }
+  return -1;
+}
+
+// The teacher over a slot list, LANES lanes per item: 4 (quad-parallel BFS) gives each query
+// the shortest dependent chain, which is what bounds a small batch; 2 (a pair, one shift
+// amount per lane) does about half the instructions per query at nearly the same chain
+// length, which is what bounds a large one; 1 does the least work but the longest chain
+// (launch_teacher picks by batch size).  DEFER (no path lengths asked): the items whose
+// answer the teacher table holds finish in the walk; the rest are listed in LDS and searched
+// by the workgroup's lane groups densely, one query each, so a wave's BFS instructions serve
+// items that need them.
+template <int NW, int LANES, bool DEFER>
+__global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
+  // the task tables in LDS: the hint-tree walk reads them in a dependent chain
+  __shared__ uint16_t s_tab[CRAFT_MAX_TASKS];
+  __shared__ int32_t s_sub[CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS];
+  __shared__ uint32_t s_work[256 / LANES];
+  __shared__ uint32_t s_nwork;
+  for (int t = threadIdx.x; t < v.n_tasks * CRAFT_MAX_SUBTASKS; t += blockDim.x) {
+    if (t < v.n_tasks) s_tab[t] = v.task_tab[t];
+    s_sub[t] = v.task_sub[t];
+  }
+  if (DEFER && threadIdx.x == 0) s_nwork = 0u;
+  __syncthreads();
+  constexpr int IPB = 256 / LANES;       // items per workgroup
+  const int g = (int)threadIdx.x / LANES, ql = (int)(threadIdx.x % LANES);
+  const int64_t i = (int64_t)blockIdx.x * IPB + g;
+  int kind = -1;
+  if (i < a.n) kind = teach_item<NW, LANES, DEFER>(v, a, i, ql, s_tab, s_sub);   // group-uniform
+  if constexpr (DEFER) {
+    if (kind >= 0 && ql == 0)
+      s_work[__hip_atomic_fetch_add(&s_nwork, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
+          (uint32_t)g | ((uint32_t)kind << 8);
+    __syncthreads();
+    if (g < (int)s_nwork) {
+      const uint32_t wk = s_work[g];
+      const int64_t ii = (int64_t)blockIdx.x * IPB + (wk & 0xffu);
+      const int64_t slot = a.slots ? (int64_t)a.slots[ii] : ii;
+      const Agent s = unpack_state(v.state[slot]);
+      const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+      const uint32_t m[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+      const int C = v.C, H = v.H;
+      const Bits<NW> valid = brange<NW>(0, C - 2 * H);
+      Bits<NW> occ, tgt;
+      band_bits<NW, LANES>(reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS), (C + 3) >> 2, C, H, m,
+                           (wk >> 8) & 0xffu, ql, occ, tgt);
+      int fa = -1, len = -1, err = 0;
+      const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y - H, s.dir, ql, fa, len, true,
+                                             v.pool_conn[s.scen] != 0);
+      const int action = go_leaf_action(ok, fa, len, err);
+      if (ql == 0) {
+        if (err) latch_error(v.err, err, slot);
+        a.act_out[ii] = action;
+      }
     }
   }
 }
@@ -266,17 +312,24 @@ hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const 
   }();
   const int lanes = forced ? forced : (n <= kTeacherQuadMaxItems ? 4 : 2);
   const unsigned blocks = (unsigned)((lanes * n + 255) / 256);
-#define CRAFT_TEACH(NWV)                                                                               \
-  do {                                                                                                 \
-    if (lanes == 4) hipLaunchKernelGGL((teacher_kernel<NWV, 4>), dim3(blocks), dim3(256), 0, st, v, a); \
-    else if (lanes == 2) hipLaunchKernelGGL((teacher_kernel<NWV, 2>), dim3(blocks), dim3(256), 0, st, v, a); \
-    else hipLaunchKernelGGL((teacher_kernel<NWV, 1>), dim3(blocks), dim3(256), 0, st, v, a);           \
+  // without path lengths the table's answers finish in the walk and the rest run densely
+#define CRAFT_TEACH_D(NWV, D)                                                                             \
+  do {                                                                                                    \
+    if (lanes == 4) hipLaunchKernelGGL((teacher_kernel<NWV, 4, D>), dim3(blocks), dim3(256), 0, st, v, a); \
+    else if (lanes == 2) hipLaunchKernelGGL((teacher_kernel<NWV, 2, D>), dim3(blocks), dim3(256), 0, st, v, a); \
+    else hipLaunchKernelGGL((teacher_kernel<NWV, 1, D>), dim3(blocks), dim3(256), 0, st, v, a);           \
+  } while (0)
+#define CRAFT_TEACH(NWV)                         \
+  do {                                           \
+    if (len_out) CRAFT_TEACH_D(NWV, false);      \
+    else CRAFT_TEACH_D(NWV, true);               \
   } while (0)
   if (nw <= 2) CRAFT_TEACH(2);
   else if (nw <= 4) CRAFT_TEACH(4);
   else if (nw <= 5) CRAFT_TEACH(5);
   else CRAFT_TEACH(8);
 #undef CRAFT_TEACH
+#undef CRAFT_TEACH_D
   return hipGetLastError();
 }
 

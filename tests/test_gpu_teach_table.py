@@ -50,6 +50,10 @@ def test_step_teach_labels_with_and_without_table(monkeypatch, world, W, n, teac
     plen = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(2)]
     acts = [s.teacher(path_len_out=p)[0] for s, p in zip((a, b), plen)]
     assert torch.equal(acts[0], acts[1]) and torch.equal(plen[0], plen[1])
+    # without path lengths the standalone teacher defers its BFS queries to a dense pass
+    dense = [s.teacher()[0] for s in (a, b)]
+    assert torch.equal(dense[0], acts[0]) and torch.equal(dense[1], acts[0])
+    assert torch.equal(labels[0], acts[0])            # the last tick's labels are these states' labels
     a.check()
     b.check()
 
