@@ -55,6 +55,9 @@ struct SimView {
   // (tt_slot: 4 bits per kind id, 0xf = none); null when the table is off (too large)
   const uint16_t* ttab;
   int32_t tt_slots;
+  int32_t tt_fused;           // 1: the fused tick + teacher kernels read the table too (CRAFT_TT_FUSED;
+                              // 0 by default: under the tick's stores its L2 reads cost more than
+                              // the dense BFS pass they save)
   uint64_t tt_slot[2];
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
@@ -123,14 +126,17 @@ __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F, int obs
 }
 
 // The tile kernel's dynamic LDS.  With compact staging (cpt, 5x5 / 7x7 windows) the "obs" piece
-// holds the tile's compact records [tile][RS] words and then the group descriptors [F / 4] u64
-// (craft_obs.h) instead of the u8 rows [tile][F]: 57 words for a 5x5 row of 1076 bytes.
+// holds the tile's compact records [tile][RS] words (craft_obs.h) instead of the u8 rows
+// [tile][F]: the one-hot part of a row as a bit string, then its tail as bytes -- 41 words for a
+// 5x5 row of 1076 bytes.
 __host__ __device__ inline int compact_tail_words(int K) { return (K + 5 + 3) / 4; }
+__host__ __device__ inline int compact_bit_words(int win, int K) { return (2 * win * win * K + 31) / 32; }
 __host__ __device__ inline int compact_stride(int win, int K) {
-  return (2 * win * win + compact_tail_words(K) + 1) | 1;        // + 1 word read past the tail; odd
+  return (compact_bit_words(win, K) + compact_tail_words(K)) | 1;   // odd: rows spread over banks
 }
 __host__ __device__ inline int compact_obs_bytes(int tile, int win, int K, int F) {
-  return ((tile * compact_stride(win, K) * 4 + 15) & ~15) + (F / 4) * 8;
+  (void)F;
+  return (tile * compact_stride(win, K) * 4 + 15) & ~15;
 }
 __host__ __device__ inline LdsLayout tile_lds_layout(int tile, int GS, int F, bool cpt, int win, int K) {
   if (!cpt) return lds_layout(tile, GS, F);
@@ -142,9 +148,9 @@ __host__ __device__ inline LdsLayout tile_lds_layout(int tile, int GS, int F, bo
   l.inv += shift; l.task += shift; l.rc += shift; l.agent += shift; l.ctrl += shift; l.bytes += shift;
   return l;
 }
-// Whether a handle's tile kernels use compact staging: 5x5 / 7x7 windows, rows a whole number of
-// 4-value groups (F % 4 == 0) and K >= 4 (a group then spans at most two record words).
-__host__ __device__ inline bool compact_ok(int win, int K, int F) { return win >= 5 && F % 4 == 0 && K >= 4; }
+// Whether a handle's tile kernels use compact staging: 5x5 / 7x7 windows and rows a whole number
+// of 4-value groups (F % 4 == 0: an fp32 row is whole 16-byte stores).
+__host__ __device__ inline bool compact_ok(int win, int K, int F) { (void)K; return win >= 5 && F % 4 == 0; }
 
 struct TileArgs {
   const int32_t* src;

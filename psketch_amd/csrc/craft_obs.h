@@ -193,83 +193,61 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
 // ---- compact staging (5x5 / 7x7 windows, the tile kernel) ------------------------------------
 // A 5x5 features() row is 1076 bytes, so 64 u8 rows (69 KB) leave room for two tile workgroups
 // per CU and 65,536 envs run in two rounds.  Instead each env stages a record of RS words:
-//   [0, W2)        local cell c = i*WIN + j: bit k set iff the cell holds kind k (k > 0)
-//   [W2, 2*W2)     pooled block b = bi*WIN + bj: bit k set iff some cell of the block holds k
-//   [2*W2, +TW)    the row's tail as bytes: inventory counts [K], dir one-hot [4], the 0
-//   (+ padding: one word past the tail is read, never used)
-// and E reads each group of 4 consecutive features off it through a per-row descriptor table
-// (the same for every env).  Feature f < 2*W2*K lives at bit f % K of word f / K; a tail feature
-// at byte (f - 2*W2*K) of the tail.  Group q (features 4q .. 4q+3; F % 4 == 0, so groups never
-// straddle rows): bits 0-15 = word w0 of its first feature, then per feature j at 16 + 8j:
-// bit 0 = word w0 + 1 instead of w0, bits 1-5 = shift, bit 6 = a byte (else a bit).  K >= 4, so
-// a group spans at most two words.
-__device__ __forceinline__ void build_group_desc(uint64_t* desc, int W2, int K, int F, int t0, int nthr) {
-  const int L2 = 2 * W2 * K;
-  for (int q = t0; q < F / 4; q += nthr) {
-    int w[4], c[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = 4 * q + j;
-      if (f < L2) {
-        w[j] = f / K;
-        c[j] = (f - w[j] * K) << 1;
-      } else {
-        const int b = f - L2;
-        w[j] = 2 * W2 + (b >> 2);
-        c[j] = ((8 * (b & 3)) << 1) | 64;
-      }
-    }
-    uint64_t d = (uint64_t)w[0];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) d |= (uint64_t)(c[j] | (w[j] - w[0])) << (16 + 8 * j);
-    desc[q] = d;
-  }
+//   [0, NB)        the one-hot part of the row, features [0, L2 = 2*W2*K) (local, then pooled),
+//                  as a bit string: feature f is bit f % 32 of word f / 32
+//   [NB, NB + TW)  the row's tail as bytes: inventory counts [K], dir one-hot [4], the 0
+// 41 words for a 5x5 row.  A group of 4 features (one 16-byte fp32 store) below L2 is one nibble
+// of one word, so E reads one word per store and spreads the nibble into 4 bytes with a multiply;
+// only the few groups at and past L2 take the per-value path.
+struct CompactShape {
+  int L2, NB;                                   // one-hot features; bit-string words
+};
+
+__device__ __forceinline__ uint32_t compact_value(const uint32_t* rec_e, int f, CompactShape cs) {
+  if (f < cs.L2) return (rec_e[f >> 5] >> (f & 31)) & 1u;
+  const int b = f - cs.L2;
+  return (rec_e[cs.NB + (b >> 2)] >> (8 * (b & 3))) & 0xffu;
 }
 
-// The 4 feature values of group `d` of the record at rec_e, one byte each.
-__device__ __forceinline__ uint32_t group_bytes(const uint32_t* rec_e, uint64_t d) {
-  const uint32_t* r = rec_e + (uint32_t)(d & 0xffffu);
-  const uint32_t a0 = r[0], a1 = r[1];               // one ds_read2_b32
-  const uint32_t hi = (uint32_t)(d >> 16);
+// Features 4q .. 4q+3 of a record, one byte each.
+__device__ __forceinline__ uint32_t compact_group(const uint32_t* rec_e, int q, CompactShape cs) {
+  if (4 * q + 3 < cs.L2) {
+    const uint32_t nib = __builtin_amdgcn_ubfe(rec_e[q >> 3], 4u * (q & 7), 4u);
+    return (nib * 0x204081u) & 0x01010101u;     // bit j -> byte j (the four partial products
+  }                                             // occupy disjoint bits: no carries)
   uint32_t out = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t c = (hi >> (8 * j)) & 0xffu;
-    const uint32_t w = (c & 1u) ? a1 : a0;
-    out |= ((w >> ((c >> 1) & 31u)) & ((c & 64u) ? 0xffu : 1u)) << (8 * j);
-  }
+  for (int j = 0; j < 4; ++j) out |= compact_value(rec_e, 4 * q + j, cs) << (8 * j);
   return out;
 }
 
+// OR a K-bit field (bits of `m`, K <= 32) into the bit string at bit p.
+__device__ __forceinline__ void or_field(uint32_t* rec, int p, uint32_t m) {
+  const int w = p >> 5, sh = p & 31;
+  atomicOr(rec + w, m << sh);
+  const uint32_t hi = sh ? (m >> (32 - sh)) : 0u;
+  if (hi) atomicOr(rec + w + 1, hi);
+}
+
 // Phase D with compact records, one env split over P lanes (as scatter_env_part): unit 0 writes
-// the local cell masks and the tail words; unit 1 + c ORs grid column c of the pooled window into
-// its blocks' masks (LDS atomics: the columns of one block share a word).  The pooled words must
-// be zero beforehand.
+// the tail words; unit 1 + c takes grid column c of the pooled window, block by block (blocks
+// wholly outside the grid skipped): its WIN cells' kind bits OR-ed into one mask, the mask OR-ed
+// into the block's K-bit field.  The local window is the pooled window's centre block
+// (x - hw .. x + hw, y - hw .. y + hw), so the centre column's units also set the local bits from
+// the same reads.  Lanes of an env share words (the local/pooled boundary, the columns of one
+// block), so every bit goes in with an LDS atomic OR; the bit string must be zero beforehand.
 template <int WIN, int P>
 __device__ __forceinline__ void scatter_env_compact(const SimView& v, const uint8_t* g, const uint8_t* iv,
-                                                    uint32_t ag, uint32_t* rec, int part) {
+                                                    uint32_t ag, uint32_t* rec, int NB, int part) {
   const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
   const int W = v.W, H = v.H, K = v.K;
   constexpr int W2 = WIN * WIN, hw = WIN / 2, bh = W2 / 2;
-  constexpr int NR = W2 < CRAFT_MAX_DIM ? W2 : CRAFT_MAX_DIM;
+  const int L = W2 * K;
   const int cxa = max(x - bh, 0), cxb = min(x - bh + W2 - 1, W - 1);
-  const int cya = max(y - bh, 0), cyb = min(y - bh + W2 - 1, H - 1);
   const int nc = cxb - cxa + 1;
 #pragma unroll 1
   for (int unit = part; unit <= nc; unit += P) {
     if (unit == 0) {
-      int kk[W2];
-#pragma unroll
-      for (int i = 0; i < WIN; ++i)
-#pragma unroll
-        for (int j = 0; j < WIN; ++j) {
-          const int cx = x - hw + i, cy = y - hw + j;
-          const bool ok = (unsigned)cx < (unsigned)W && (unsigned)cy < (unsigned)H;
-          const int k = g[min(max(cx, 0), W - 1) * H + min(max(cy, 0), H - 1)];
-          kk[i * WIN + j] = ok ? k : 0;
-        }
-#pragma unroll
-      for (int c = 0; c < W2; ++c) rec[c] = kk[c] ? (1u << kk[c]) : 0u;
       // the tail: inventory bytes [0, K) (tail word t is inventory word t, its bytes past K
       // cleared), the dir one-hot at byte K + dir, then zeros (K <= 32: at most 10 words)
       const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);
@@ -280,31 +258,38 @@ __device__ __forceinline__ void scatter_env_compact(const SimView& v, const uint
           const int nb = min(max(K - 4 * t, 0), 4);                   // inventory bytes in word t
           uint32_t o = t < 8 ? (ivw[t] & (nb == 4 ? ~0u : (1u << (8 * nb)) - 1u)) : 0u;
           o |= ((db >> 2) == t) ? (1u << (8 * (db & 3))) : 0u;
-          rec[2 * W2 + t] = o;
+          rec[NB + t] = o;
         }
       }
     } else {
       const int cx = cxa + unit - 1;
       const int bi = (cx - x + bh) / WIN;
+      const int li = cx - x + hw;                                     // local row, if in [0, WIN)
       const uint8_t* col = g + cx * H;
-      int kk[NR];
 #pragma unroll
-      for (int j = 0; j < NR; ++j) kk[j] = col[min(cya + j, H - 1)];
-      uint32_t m[WIN];
+      for (int b = 0; b < WIN; ++b) {
+        const int cy0 = y - bh + b * WIN;
+        if (cy0 >= H || cy0 + WIN <= 0) continue;                     // the block is padding
+        int kk[WIN];
+        uint32_t m = 0;
 #pragma unroll
-      for (int b = 0; b < WIN; ++b) m[b] = 0;
+        for (int jj = 0; jj < WIN; ++jj) {                            // unconditional reads, masked
+          const int cy = cy0 + jj;
+          const int k = col[min(max(cy, 0), H - 1)];
+          kk[jj] = (unsigned)cy < (unsigned)H ? k : 0;
+          m |= 1u << kk[jj];
+        }
+        m &= ~1u;                                                     // kind 0 = empty
+        if (m) or_field(rec, L + (bi * WIN + b) * K, m);
+        if (b == hw && (unsigned)li < (unsigned)WIN) {                // the local window's column
 #pragma unroll
-      for (int j = 0; j < NR; ++j) {
-        const int cy = cya + j;
-        const uint32_t bit = (cy <= cyb && kk[j]) ? (1u << kk[j]) : 0u;
-        const int bj = (cy - y + bh) / WIN;
-#pragma unroll
-        for (int b = 0; b < WIN; ++b) m[b] |= (b == bj) ? bit : 0u;
+          for (int jj = 0; jj < WIN; ++jj)
+            if (kk[jj]) {
+              const int f = ((li * WIN) + jj) * K + kk[jj];
+              atomicOr(rec + (f >> 5), 1u << (f & 31));
+            }
+        }
       }
-      uint32_t* brow = rec + W2 + bi * WIN;
-#pragma unroll
-      for (int b = 0; b < WIN; ++b)
-        if (m[b]) atomicOr(brow + b, m[b]);
     }
   }
 }
@@ -316,7 +301,8 @@ __device__ __forceinline__ void scatter_compact(const SimView& v, const uint8_t*
   const int e = tid % TILE, part = tid / TILE;
   const uint32_t ag = s_agent[e];
   if (e < nE && (ag >> 24))
-    scatter_env_compact<WIN, kParts>(v, s_grid + e * v.GS, s_inv + e * kInvStride, ag, s_rec + e * RS, part);
+    scatter_env_compact<WIN, kParts>(v, s_grid + e * v.GS, s_inv + e * kInvStride, ag, s_rec + e * RS,
+                                     compact_bit_words(WIN, v.K), part);
 }
 
 // 16 bytes of output from four packed feature-byte words (as pack16 on the u8 rows).
@@ -335,65 +321,13 @@ __device__ __forceinline__ obs_vec pack_bytes(const uint32_t* b) {
   }
 }
 
-// One feature value of a record pair (a0, a1) = rec[w0], rec[w0 + 1] by its descriptor byte c.
-__device__ __forceinline__ uint32_t desc_value(uint32_t a0, uint32_t a1, uint32_t c) {
-  return __builtin_amdgcn_ubfe((c & 1u) ? a1 : a0, (c >> 1) & 31u, (c & 64u) ? 8u : 1u);
-}
-
-// Phase E, fp32, compact records: every 16-byte store is one group of 4 features (F % 4 == 0,
-// rows 16-byte aligned).  Thread t owns group q = t (+ NTHR, ...) of every row: it decodes the
-// group's descriptor once, then per row reads its two record words and extracts 4 values (one
-// bit-field extract each), so a store costs ~15 instructions.  Consecutive lanes store
-// consecutive groups of one row (contiguous).  The G % NTHR groups left over go round flat.
-template <int NTHR = kThreads>
-__device__ __forceinline__ void stream_compact_f32(const uint32_t* s_rec, const uint64_t* s_desc, void* obs,
-                                                   int64_t env0, int F, int RS, int nE, int policy, int tid) {
-  const int G = F >> 2;
-  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * 4;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, nE * F * 4, 0x00020000);
-  auto put = [&](const obs_vec& o, int off) {
-    if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, off, 0, 2);          // nt
-    else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, off, 0, 16);    // sc1
-    else __builtin_amdgcn_raw_buffer_store_b128(o, rsrc, off, 0, 0);
-  };
-  auto vals = [&](uint32_t a0, uint32_t a1, uint32_t hi) {
-    return obs_vec{__float_as_uint((float)desc_value(a0, a1, hi & 0xffu)),
-                   __float_as_uint((float)desc_value(a0, a1, (hi >> 8) & 0xffu)),
-                   __float_as_uint((float)desc_value(a0, a1, (hi >> 16) & 0xffu)),
-                   __float_as_uint((float)desc_value(a0, a1, hi >> 24))};
-  };
-  const int full = G / NTHR;
-  for (int r = 0; r < full; ++r) {
-    const int q = tid + r * NTHR;
-    const uint64_t d = s_desc[q];
-    const uint32_t hi = (uint32_t)(d >> 16);
-    const uint32_t* rp = s_rec + (uint32_t)(d & 0xffffu);
-    constexpr int U = 4;                               // stores in flight per lane
-    for (int e = 0; e < nE; e += U) {
-      obs_vec o[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (e + u < nE) o[u] = vals(rp[(e + u) * RS], rp[(e + u) * RS + 1], hi);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (e + u < nE) put(o[u], ((e + u) * G + q) * 16);
-    }
-  }
-  const int R = G - full * NTHR;                       // groups left over, every row
-  for (int f = tid; f < R * nE; f += NTHR) {
-    const int e = f / R, q = full * NTHR + (f - e * R);
-    const uint64_t d = s_desc[q];
-    const uint32_t* rp = s_rec + e * RS + (uint32_t)(d & 0xffffu);
-    put(vals(rp[0], rp[1], (uint32_t)(d >> 16)), (e * G + q) * 16);
-  }
-}
-
-// Phase E with compact records: the tile's rows as one flat stream of 16-byte stores (as
-// stream_obs), each store's 4 / 8 / 16 values read off the records by group descriptor (the
-// bf16 / u8 formats, whose stores may straddle rows; fp32 takes stream_compact_f32).
+// Phase E with compact records: the tile's rows as one flat stream of 16-byte stores, exactly as
+// stream_obs streams the u8 rows (consecutive lanes, consecutive 16 bytes: every wave store is
+// whole cache lines), each store's 4 / 8 / 16 values read off the records one group at a time.
+// The lane's group is tracked as (row e, group q) and advanced, never divided.
 template <int FMT, int NTHR = kThreads>
-__device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint64_t* s_desc, void* obs,
-                                               int64_t env0, int F, int RS, int nE, int policy, int tid) {
+__device__ __forceinline__ void stream_compact(const uint32_t* s_rec, void* obs, int64_t env0, int F, int RS,
+                                               CompactShape cs, int nE, int policy, int tid) {
   constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
   constexpr int PER = 16 / ESZ;                // values per 16-byte store
   constexpr int GPS = PER / 4;                 // groups per store
@@ -403,8 +337,6 @@ __device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint
   uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
   constexpr int U = 4;
-  // the lane's group gg = sidx * GPS + j as (row e, group q), advanced by NTHR * GPS groups per
-  // store slot instead of divided each time
   int ge = (tid * GPS) / G, gq = tid * GPS - ge * G;
   for (int base = tid; base < nv; base += U * NTHR) {
     obs_vec o[U];
@@ -416,8 +348,8 @@ __device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint
         int e = ge, q = gq;
 #pragma unroll
         for (int j = 0; j < GPS; ++j) {
-          b[j] = group_bytes(s_rec + e * RS, s_desc[q]);
-          if (++q == G) { q = 0; ++e; }
+          b[j] = compact_group(s_rec + e * RS, q, cs);
+          if (GPS > 1 && ++q == G) { q = 0; ++e; }
         }
         o[u] = pack_bytes<FMT>(b);
       }
@@ -436,7 +368,7 @@ __device__ __forceinline__ void stream_compact(const uint32_t* s_rec, const uint
   }
   for (int f = nv * PER + tid; f < total; f += NTHR) {       // the last few values of the tile
     const int e = f / F, ff = f - e * F;
-    const uint32_t bt = (group_bytes(s_rec + e * RS, s_desc[ff >> 2]) >> (8 * (ff & 3))) & 0xffu;
+    const uint32_t bt = compact_value(s_rec + e * RS, ff, cs);
     if (FMT == CRAFT_OBS_F32) reinterpret_cast<float*>(tile_out)[f] = (float)bt;
     else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint16_t*>(tile_out)[f] = (uint16_t)(__float_as_uint((float)bt) >> 16);
     else tile_out[f] = (uint8_t)bt;

@@ -313,7 +313,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   // stats rows: one per 16-env tile, plus the step kernel's last workgroup's tick waves (its
   // wave count is rounded up to the workgroup's 4)
   s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs + 4;
-  // default tile: 64 envs (3x3 rows, 5x5 compact records: ~30 KB, 4 workgroups per CU), 32 for
+  // default tile: 64 envs (3x3 rows, 5x5 compact records: ~22 KB at 12x12, 4 workgroups per CU), 32 for
   // 7x7 compact records; without compact staging the u8 rows stay near 40 KB per workgroup
   // (CRAFT_COMPACT=0 at creation: the u8 rows instead, a diagnostic for the A/B and parity tests)
   const char* cpt_env = getenv("CRAFT_COMPACT");
@@ -322,6 +322,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   s->tile = default_tile(cfg->window_width, s->view.cpt != 0);
   const char* prio_env = getenv("CRAFT_T2_PRIO");
   s->view.t2_prio = prio_env ? atoi(prio_env) : 0;
+  const char* ttf_env = getenv("CRAFT_TT_FUSED");
+  s->view.tt_fused = ttf_env ? (atoi(ttf_env) != 0) : 0;
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks

@@ -341,10 +341,11 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
         s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int len = -1, err = 0, defer = -1;
-        // the hint walk, and the teacher table for a pristine grid; a BFS left over is deferred
+        // the hint walk (and, with tt_fused, the teacher table for a pristine grid); a BFS left
+        // over is deferred to the workgroup's dense pass
         action = teach_env<NW, TL, true>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + le * GS), m0,
                                    s_inv + le * kInvStride, s, s.task, ql, false, len, err,
-                                   ((ti >> 9) & 1u) != 0, ((ti >> 10) & 1u) ? tt_row(v, (int)(ti >> 11)) : nullptr,
+                                   ((ti >> 9) & 1u) != 0, (v.tt_fused && ((ti >> 10) & 1u)) ? tt_row(v, (int)(ti >> 11)) : nullptr,
                                    &defer);
         if (err && ql == 0) latch_error(v.err, err, i);
         if (action == kTeachDeferred && ql == 0)

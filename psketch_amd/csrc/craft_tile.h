@@ -32,8 +32,8 @@ namespace craft {
 template <int WIN, int MODE, int TILE, int TL = 0, int NW = 0>
 __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) void tile_kernel(SimView v, TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // compact staging (craft_obs.h) for 5x5 / 7x7 windows: records + group descriptors in place of
-  // the u8 rows, so a 64-env tile fits 4 workgroups per CU (the host sets v.cpt, compact_ok)
+  // compact staging (craft_obs.h) for 5x5 / 7x7 windows: bit-string records in place of the u8
+  // rows, so a 64-env tile fits 4 workgroups per CU (the host sets v.cpt, compact_ok)
   constexpr bool kCptWin = WIN >= 5;
   const bool cpt = kCptWin && v.cpt;
   const LdsLayout lay = tile_lds_layout(TILE, v.GS, v.F, cpt, WIN, v.K);
@@ -41,7 +41,6 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
   uint8_t* s_grid = smem;
   uint8_t* s_obs = smem + lay.obs;
   uint32_t* s_rec = reinterpret_cast<uint32_t*>(s_obs);
-  uint64_t* s_desc = reinterpret_cast<uint64_t*>(s_obs + ((TILE * RS * 4 + 15) & ~15));
   uint8_t* s_inv = smem + lay.inv;
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
@@ -306,11 +305,9 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
       }
     }
   } else if (want_obs && tid < kThreads) {
-    // waves 1-3: zero the tile's observation bytes (compact: its records, and build the group
-    // descriptors) while wave 0 runs A + C
+    // waves 1-3: zero the tile's observation bytes (compact: its records) while wave 0 runs A + C
     if (kCptWin && cpt) {
       for (int i = tid - TILE; i < TILE * RS; i += kThreads - TILE) s_rec[i] = 0u;
-      build_group_desc(s_desc, WIN * WIN, v.K, F, tid - TILE, kThreads - TILE);
     } else {
       uint4* z = reinterpret_cast<uint4*>(s_obs);
       const int n16 = (nE * F + 15) >> 4;
@@ -362,10 +359,11 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
         s.x = ag & 0xff; s.y = (ag >> 8) & 0xff; s.dir = (ag >> 16) & 3; s.task = ti & 0xff;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         int len = -1, err = 0, defer = -1;
-        // the hint walk, and the teacher table for a pristine grid; a BFS left over is deferred
+        // the hint walk (and, with tt_fused, the teacher table for a pristine grid); a BFS left
+        // over is deferred to the workgroup's dense pass
         action = teach_env<NW, TL, true>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS),
                                    m0, s_inv + e * kInvStride, s, s.task, ql, false, len, err,
-                                   ((ti >> 9) & 1u) != 0, ((ti >> 10) & 1u) ? tt_row(v, (int)(ti >> 11)) : nullptr,
+                                   ((ti >> 9) & 1u) != 0, (v.tt_fused && ((ti >> 10) & 1u)) ? tt_row(v, (int)(ti >> 11)) : nullptr,
                                    &defer);
         if (err && ql == 0) latch_error(v.err, err, i);
         if (action == kTeachDeferred && ql == 0)
@@ -393,10 +391,11 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
 
   // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
   if (kCptWin && cpt) {
+    const CompactShape cs{2 * WIN * WIN * v.K, compact_bit_words(WIN, v.K)};
     switch (v.obs_fmt) {
-      case CRAFT_OBS_BF16: stream_compact<CRAFT_OBS_BF16>(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
-      case CRAFT_OBS_U8: stream_compact<CRAFT_OBS_U8>(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
-      default: stream_compact_f32(s_rec, s_desc, a.obs, env0, F, RS, nE, v.obs_policy, tid); break;
+      case CRAFT_OBS_BF16: stream_compact<CRAFT_OBS_BF16>(s_rec, a.obs, env0, F, RS, cs, nE, v.obs_policy, tid); break;
+      case CRAFT_OBS_U8: stream_compact<CRAFT_OBS_U8>(s_rec, a.obs, env0, F, RS, cs, nE, v.obs_policy, tid); break;
+      default: stream_compact<CRAFT_OBS_F32>(s_rec, a.obs, env0, F, RS, cs, nE, v.obs_policy, tid); break;
     }
     STAMP_END();
     return;

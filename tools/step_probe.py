@@ -24,6 +24,10 @@ def main():
     p.add_argument("--ring", type=int, nargs="+", default=[16, 1])
     p.add_argument("--iters", type=int, default=200)
     p.add_argument("--teacher", action="store_true")
+    p.add_argument("--tiles", type=int, nargs="+", default=[0],
+                   help="envs per tile workgroup to time the tick kernel at (0 = the handle's default)")
+    p.add_argument("--caps", type=int, nargs="+", default=[0],
+                   help="resident workgroups per CU (craft_sim_tune; 0 = as many as fit)")
     p.add_argument("--obs-store", type=int, nargs="+", default=[1],
                    help="observation store policies to time (craft_sim_tune: 0 wb, 1 nt, 2 sc1)")
     args = p.parse_args()
@@ -72,8 +76,11 @@ def main():
 
         res = {"world": args.world, "envs": n, "ring": R, "fill_us": round(timeit(fill, args.iters), 2)}
         for pol in args.obs_store:
-            sim.tune(0, 0, pol)
-            res[f"tile_p{pol}_us"] = round(timeit(step, args.iters), 2)
+            for tl in args.tiles:
+                for cap in args.caps:
+                    sim.tune(tl, cap, pol)
+                    key = "tile" + (f"{tl}" if tl else "") + (f"_cap{cap}" if cap else "")
+                    res[f"{key}_p{pol}_us"] = round(timeit(step, args.iters), 2)
         sim.tune(0, 0, 2)
         if args.teacher:
             for pol in args.obs_store:
