@@ -684,4 +684,17 @@ __device__ __forceinline__ void teach_deferred(const SimView& v, const uint32_t*
   }
 }
 
+// The dense pass over NT teacher threads (thread u of them) with the widest lane groups the count
+// allows: quads, the BFS's shortest dependent chain, when the n queries fit one per quad, else
+// the kernel's own LANES (n is workgroup-uniform, so is the branch).
+template <int NW, int LANES>
+__device__ __forceinline__ void teach_deferred_dense(const SimView& v, const uint32_t* work, int n, int u, int NT,
+                                                     const uint8_t* s_grid, int GS, const uint32_t* s_agent,
+                                                     const uint32_t* s_info, int32_t* label, int64_t env0) {
+  if (LANES < 4 && n <= NT / 4)
+    teach_deferred<NW, 4>(v, work, n, u >> 2, NT / 4, u & 3, s_grid, GS, s_agent, s_info, label, env0);
+  else
+    teach_deferred<NW, LANES>(v, work, n, u / LANES, NT / LANES, u % LANES, s_grid, GS, s_agent, s_info, label, env0);
+}
+
 }  // namespace craft

@@ -88,6 +88,33 @@ __device__ __forceinline__ int teach_item(const SimView& v, const TeachArgs& a, 
   return -1;
 }
 
+// One deferred item of the teacher kernel's dense pass (lane group g of L lanes takes list entry
+// g): its go[X] BFS on the env's current grid, read from HBM as teach_item does.
+template <int NW, int L>
+__device__ __forceinline__ void dense_item(const SimView& v, const TeachArgs& a, const uint32_t* s_work, int n, int g,
+                                           int ql, int ipb) {
+  if (g >= n) return;
+  const uint32_t wk = s_work[g];
+  const int64_t ii = (int64_t)blockIdx.x * ipb + (wk & 0xffu);
+  const int64_t slot = a.slots ? (int64_t)a.slots[ii] : ii;
+  const Agent s = unpack_state(v.state[slot]);
+  const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+  const uint32_t m[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+  const int C = v.C, H = v.H;
+  const Bits<NW> valid = brange<NW>(0, C - 2 * H);
+  Bits<NW> occ, tgt;
+  band_bits<NW, L>(reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS), (C + 3) >> 2, C, H, m,
+                   (wk >> 8) & 0xffu, ql, occ, tgt);
+  int fa = -1, len = -1, err = 0;
+  const bool ok = bfs_closest<NW, L>(occ, tgt, valid, H, s.x * H + s.y - H, s.dir, ql, fa, len, true,
+                                     v.pool_conn[s.scen] != 0);
+  const int action = go_leaf_action(ok, fa, len, err);
+  if (ql == 0) {
+    if (err) latch_error(v.err, err, slot);
+    a.act_out[ii] = action;
+  }
+}
+
 // The teacher over a slot list, LANES lanes per item: 4 (quad-parallel BFS) gives each query
 // the shortest dependent chain, which is what bounds a small batch; 2 (a pair, one shift
 // amount per lane) does about half the instructions per query at nearly the same chain
@@ -119,27 +146,10 @@ __global__ __launch_bounds__(256) void teacher_kernel(SimView v, TeachArgs a) {
       s_work[__hip_atomic_fetch_add(&s_nwork, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
           (uint32_t)g | ((uint32_t)kind << 8);
     __syncthreads();
-    if (g < (int)s_nwork) {
-      const uint32_t wk = s_work[g];
-      const int64_t ii = (int64_t)blockIdx.x * IPB + (wk & 0xffu);
-      const int64_t slot = a.slots ? (int64_t)a.slots[ii] : ii;
-      const Agent s = unpack_state(v.state[slot]);
-      const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
-      const uint32_t m[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-      const int C = v.C, H = v.H;
-      const Bits<NW> valid = brange<NW>(0, C - 2 * H);
-      Bits<NW> occ, tgt;
-      band_bits<NW, LANES>(reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS), (C + 3) >> 2, C, H, m,
-                           (wk >> 8) & 0xffu, ql, occ, tgt);
-      int fa = -1, len = -1, err = 0;
-      const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, H, s.x * H + s.y - H, s.dir, ql, fa, len, true,
-                                             v.pool_conn[s.scen] != 0);
-      const int action = go_leaf_action(ok, fa, len, err);
-      if (ql == 0) {
-        if (err) latch_error(v.err, err, slot);
-        a.act_out[ii] = action;
-      }
-    }
+    const int nwk = (int)s_nwork;
+    // quads (the shortest BFS chain) when every deferred item fits one per quad
+    if (LANES < 4 && nwk <= 64) dense_item<NW, 4>(v, a, s_work, nwk, (int)threadIdx.x >> 2, (int)threadIdx.x & 3, IPB);
+    else dense_item<NW, LANES>(v, a, s_work, nwk, g, ql, IPB);
   }
 }
 

@@ -85,10 +85,18 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   // stores, 6 the last teacher wave done, 7 the XCC.  With CRAFT_STAMPS_C, wave 0's A + C in
   // detail instead: 1 the state word landed, 2 the pool row in LDS, 3 the pre-step tests and
   // cleared cells applied, 4 the transition done, 5 its global stores issued, 6 C done.
+  // With CRAFT_STAMPS_T, the teacher in detail instead: 1 the last teacher wave's walk done, 2
+  // the last teacher wave into the dense pass, 4 the number of deferred queries (a count).
 #ifdef CRAFT_STAMPS_C
 #define T2S(k, kc) do { if ((kc) >= 0) STAMP((kc) < 0 ? 0 : (kc)); } while (0)
 #define T2SM(k) do {} while (0)
+#define T2ST(k) do {} while (0)
+#elif defined(CRAFT_STAMPS_T)
+#define T2S(k, kc) do { if ((k) == 3) STAMP(3); } while (0)
+#define T2SM(k) STAMP_MAX(k)
+#define T2ST(k) STAMP_MAX(k)
 #else
+#define T2ST(k) do {} while (0)
 #define T2S(k, kc) do { if ((k) >= 0) STAMP((k) < 0 ? 0 : (k)); } while (0)
 #define T2SM(k) STAMP_MAX(k)
 #endif
@@ -355,18 +363,24 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       if (ql == 0 && action != kTeachDeferred) a.label[i] = action;
     }
     // every teacher wave has listed its deferred queries; then all of them run the BFS densely
+    T2ST(1);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if ((tid & 63) == 0) __hip_atomic_fetch_add(&s_wctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     while (__hip_atomic_load(&s_wctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)(J * TL))
       __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const uint32_t nw = __hip_atomic_load(&s_wctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    teach_deferred<NW, TL>(v, s_work, (int)nw, u / TL, J * kTick2Tile, ql, s_grid, GS, s_agent, s_tinfo,
-                           a.label + envw, envw);
+    T2ST(2);
+#ifdef CRAFT_STAMPS_T
+    if (u == 0 && v.stamps) v.stamps[8 * (int64_t)blockIdx.x + 4] = nw;
+#endif
+    teach_deferred_dense<NW, TL>(v, s_work, (int)nw, u, J * kTick2Tile * TL, s_grid, GS, s_agent, s_tinfo,
+                                 a.label + envw, envw);
     T2SM(6);
   }
 }
 #undef T2S
 #undef T2SM
+#undef T2ST
 
 }  // namespace craft

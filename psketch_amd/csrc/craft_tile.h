@@ -379,8 +379,8 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
       __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const uint32_t nw = __hip_atomic_load(&s_wctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    teach_deferred<NW, TL>(v, s_work, (int)nw, u / TL, TILE, ql, s_grid, v.GS, s_agent, s_tinfo, a.label + env0,
-                           env0);
+    teach_deferred_dense<NW, TL>(v, s_work, (int)nw, u, TILE * TL, s_grid, v.GS, s_agent, s_tinfo, a.label + env0,
+                                 env0);
     STAMP_END();
     return;
   }

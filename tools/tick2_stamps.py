@@ -5,6 +5,7 @@ wave 0's first store issued, the last tick wave done issuing stores, and the las
 done; whether the BFS or the stores end each workgroup; and the XCC histogram.
 
     python tools/diag_build.py craft_sim craft_tick_teach      # here (CPU)
+    python tools/diag_build.py craft_sim craft_tick_teach -DCRAFT_STAMPS_T --out libpsketch_craft_diag_t.so
     python tools/tick2_stamps.py [--ring 16|1] [--ticks 30]    # on the GPU box"""
 import argparse
 import ctypes
@@ -25,7 +26,8 @@ def main():
     p.add_argument("--ring", type=int, nargs="+", default=[16, 1])
     p.add_argument("--ticks", type=int, default=30)
     p.add_argument("--lib", default="libpsketch_craft_diag.so",
-                   help="diagnostic library; libpsketch_craft_diag_c.so (-DCRAFT_STAMPS_C): wave 0's A + C")
+                   help="diagnostic library; libpsketch_craft_diag_c.so (-DCRAFT_STAMPS_C): wave 0's A + C; "
+                        "libpsketch_craft_diag_t.so (-DCRAFT_STAMPS_T): the teacher's walk and dense pass")
     args = p.parse_args()
     import torch
     from psketch_amd import _native
@@ -47,6 +49,9 @@ def main():
     if "diag_c" in args.lib:             # CRAFT_STAMPS_C: wave 0's A + C in detail
         names = ["start", "state_landed", "row_in_lds", "pre_step_done", "transition_done", "stores_issued",
                  "C_done"]
+    tmode = "diag_t" in args.lib        # CRAFT_STAMPS_T: the teacher's walk, the dense pass, the count
+    if tmode:
+        names = ["start", "walk_done", "dense_start", "barrier", "deferred", "stores_issued", "teacher_done"]
     for R in args.ring:
         ring = [sim.empty_obs() for _ in range(R)]
         lab = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -56,7 +61,8 @@ def main():
             sim.step(seed=0, tick=t, obs=ring[t % R], labels=lab)
             torch.cuda.synchronize()
             s = st.cpu().numpy().astype(np.float64)
-            s[:, :7] = (s[:, :7] - s[:, 0].min()) / 100.0          # 100 MHz -> µs
+            tcols = [0, 1, 2, 3, 5, 6] if tmode else list(range(7))
+            s[:, tcols] = (s[:, tcols] - s[:, 0].min()) / 100.0     # 100 MHz -> µs
             rows.append(s)
         r = np.stack(rows[5:])                                     # [ticks, wgs, 8]
         out = {"world": args.world, "envs": n, "ring": R, "kernel": kname, "envs_per_wg": per_wg,
