@@ -102,7 +102,7 @@ uint64_t pack_state(const Agent& a) {
 inline int dir_dx(int d) { return d == CRAFT_LEFT ? -1 : (d == CRAFT_RIGHT ? 1 : 0); }
 inline int dir_dy(int d) { return d == CRAFT_DOWN ? -1 : (d == CRAFT_UP ? 1 : 0); }
 
-int default_tile(int win) { return win == 3 ? 64 : (win == 5 ? 64 : 32); }
+int default_tile(int win) { return win == 3 ? 64 : 32; }     // as the HIP library's (u8 rows)
 
 }  // namespace
 

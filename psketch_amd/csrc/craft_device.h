@@ -55,9 +55,8 @@ struct SimView {
   // (tt_slot: 4 bits per kind id, 0xf = none); null when the table is off (too large)
   const uint16_t* ttab;
   int32_t tt_slots;
-  int32_t tt_fused;           // 1: the fused tick + teacher kernels read the table too (CRAFT_TT_FUSED;
-                              // 0 by default: under the tick's stores its L2 reads cost more than
-                              // the dense BFS pass they save)
+  int32_t tt_fused;           // 1 (default): the fused tick + teacher kernels read the table too
+                              // (CRAFT_TT_FUSED=0 at creation: they defer every go[X] BFS instead)
   uint64_t tt_slot[2];
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
@@ -287,9 +286,17 @@ __device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, b
   return dy < 0 ? CRAFT_DOWN : dy > 0 ? CRAFT_UP : dx < 0 ? CRAFT_LEFT : CRAFT_RIGHT;
 }
 
+// RCV: the recipe words also sit in a VGPR, lane w holding word w (w < 3 * CRAFT_MAX_RECIPES,
+// loaded while every lane of the wave was active); the recipe loop reads them with v_readlane
+// instead of one LDS round trip per recipe.
+template <bool RCV = false>
 __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
-                                           bool& mask_changed) {
+                                           bool& mask_changed, uint32_t rcv = 0u) {
+  auto rword = [&](int w) -> uint32_t {
+    if constexpr (RCV) return __builtin_amdgcn_readlane(rcv, w);
+    else return __builtin_amdgcn_readfirstlane(rc[w]);
+  };
   const int H = v.H;
   int dx = 0, dy = 0, ndir = s.dir;
   if (a < CRAFT_USE) {                               // moves always turn (craft.py:341-352)
@@ -312,15 +319,15 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
           inv_changed = mask_changed = true;
 #ifndef CRAFT_ABL_NORECIPE
         } else if (cls == CRAFT_KIND_WORKSHOP) {     // recipes in dict order, craft.py:388-401
-          // Recipe words are wave-uniform (LDS broadcast reads, kept in scalar registers); a
-          // recipe's ingredient counts are read together, so a matching recipe costs two LDS
-          // round trips.  Recipes chain (a product may be the next one's ingredient): each reads
+          // Recipe words are wave-uniform (LDS broadcast reads or v_readlane, kept in scalar
+          // registers); a recipe's ingredient counts are read together, so a matching recipe
+          // costs one or two LDS round trips.  Recipes chain (a product may be the next one's ingredient): each reads
           // the inventory after the previous one's writes (LDS is in order).
           for (int r = 0; r < v.n_recipes; ++r) {
-            const uint32_t a0 = __builtin_amdgcn_readfirstlane(rc[3 * r]);
+            const uint32_t a0 = rword(3 * r);
             if ((int)((a0 >> 8) & 0xff) != thing) continue;     // the recipe's workshop
-            const uint32_t a1 = __builtin_amdgcn_readfirstlane(rc[3 * r + 1]);
-            const uint32_t a2 = __builtin_amdgcn_readfirstlane(rc[3 * r + 2]);
+            const uint32_t a1 = rword(3 * r + 1);
+            const uint32_t a2 = rword(3 * r + 2);
             const int n_in = (a0 >> 16) & 0xff;
             const int k0 = a0 >> 24, k1 = (a1 >> 8) & 0xff, k2 = a1 >> 24, k3 = (a2 >> 8) & 0xff;
             const int c0 = a1 & 0xff, c1 = (a1 >> 16) & 0xff, c2 = a2 & 0xff, c3 = (a2 >> 16) & 0xff;

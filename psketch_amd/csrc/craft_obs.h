@@ -33,7 +33,7 @@ __device__ __forceinline__ obs_vec pack16(const uint8_t* s_obs, int sidx) {
 // descriptor); the cache policy is a tuning knob (craft_sim_tune).  NTHR threads
 // (tid in [0, NTHR)) share the stream; with ZERO they also clear every byte they
 // read, leaving the rows zeroed for the next scatter.
-template <int FMT, int NTHR = kThreads, bool ZERO = false>
+template <int FMT, int NTHR = kThreads, bool ZERO = false, int U = 4>
 __device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t env0, int F, int nE,
                                            int policy, int tid) {
   constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
@@ -42,7 +42,7 @@ __device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t en
   const int nv = total / PER;
   uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
-  constexpr int U = 4;                         // independent 16-byte stores in flight per lane
+  // U: independent 16-byte stores in flight per lane
   for (int base = tid; base < nv; base += U * NTHR) {
     obs_vec o[U];
 #pragma unroll

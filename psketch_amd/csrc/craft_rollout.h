@@ -84,6 +84,9 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
 #define PACC(q, d) do {} while (0)
 #endif
   const int tid = threadIdx.x;
+  // the recipe words in a VGPR (lane w: word w), loaded while every lane is active, for the
+  // transition's recipe loop (v_readlane instead of an LDS round trip per recipe)
+  const uint32_t rcv = v.rcw[min(tid & 63, CRAFT_MAX_RECIPES * 3 - 1)];
   const int64_t n = v.n_envs;
   const bool want_obs = a.obs != nullptr;
   const int F = v.F;
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
 #ifndef CRAFT_ABL_NOTRANS
         if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-        else transition(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed);
+        else transition<true>(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed, rcv);
 #endif
         if (mask_changed) {
           const uint32_t nc = (clr >> 24) & 3;

@@ -62,6 +62,9 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
   constexpr int P = 64 / TILE;                            // scatter lanes per env
   auto up16 = [](int x) { return (x + 15) & ~15; };
   const int GS = v.GS, F = v.F;
+  // the recipe words in a VGPR (lane w: word w), loaded while every lane is active, for the
+  // transition's recipe loop (v_readlane instead of an LDS round trip per recipe)
+  const uint32_t rcv = v.rcw[min((int)(threadIdx.x & 63), CRAFT_MAX_RECIPES * 3 - 1)];
   uint8_t* s_grid = smem;                                 // [2][TILE][GS] by item parity
   uint8_t* s_pristine = smem + 2 * TILE * GS;             // [TILE][GS] pool[scenario]
   const int obs_buf = up16(TILE * F);
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_split_kernel(SimView v, Rollo
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
 #ifndef CRAFT_ABL_NOTRANS
         if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-        else transition(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed);
+        else transition<true>(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed, rcv);
 #endif
         if (mask_changed) {
           chg = 1u + (uint32_t)fc;

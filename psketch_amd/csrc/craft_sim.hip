@@ -192,7 +192,7 @@ using craft_host::validate_config;
 int default_tile(int win, bool cpt) {
   if (win == 3) return 64;
   if (win == 5) return cpt ? 64 : 32;
-  return cpt ? 32 : 16;
+  return 32;                      // 7x7: 32-env u8 rows (67 KB) measured 3 % faster than 16 at 16x16
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -313,17 +313,17 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   // stats rows: one per 16-env tile, plus the step kernel's last workgroup's tick waves (its
   // wave count is rounded up to the workgroup's 4)
   s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs + 4;
-  // default tile: 64 envs (3x3 rows, 5x5 compact records: ~22 KB at 12x12, 4 workgroups per CU), 32 for
-  // 7x7 compact records; without compact staging the u8 rows stay near 40 KB per workgroup
-  // (CRAFT_COMPACT=0 at creation: the u8 rows instead, a diagnostic for the A/B and parity tests)
+  // default tile: 64 envs for 3x3 rows, 32 for 5x5 and 7x7 rows.  Compact records for 5x5 / 7x7
+  // windows (craft_obs.h) are an option (CRAFT_COMPACT=1 at creation: 64-env tiles for 5x5, one
+  // round of workgroups), measured slower than the u8 rows at every shape
   const char* cpt_env = getenv("CRAFT_COMPACT");
   s->view.cpt = craft::compact_ok(cfg->window_width, cfg->n_kinds, cfg->n_features) &&
-                !(cpt_env && atoi(cpt_env) == 0) ? 1 : 0;
+                (cpt_env && atoi(cpt_env) == 1) ? 1 : 0;
   s->tile = default_tile(cfg->window_width, s->view.cpt != 0);
   const char* prio_env = getenv("CRAFT_T2_PRIO");
   s->view.t2_prio = prio_env ? atoi(prio_env) : 0;
   const char* ttf_env = getenv("CRAFT_TT_FUSED");
-  s->view.tt_fused = ttf_env ? (atoi(ttf_env) != 0) : 0;
+  s->view.tt_fused = ttf_env ? (atoi(ttf_env) != 0) : 1;
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks

@@ -59,6 +59,9 @@ __host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F) {
 #ifndef CRAFT_T2_WPE
 #define CRAFT_T2_WPE 4
 #endif
+#ifndef CRAFT_T2_U
+#define CRAFT_T2_U 4            // 16-byte stores in flight per lane of a tick wave's E
+#endif
 // TW tick waves (4 or 8): D + E of 64 / TW envs per tile each.
 template <int WIN, int J, int TW, int TL, int NW>
 __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void tick2_kernel(SimView v, TileArgs a) {
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
           latch_error(v.err, CRAFT_EBADACTION, slot);
         } else {
           const int ox = s.x, oy = s.y;
-          transition(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed);
+          transition<true>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw);
           code = transition_code(ox, oy, s, inv_changed);
         }
       }
@@ -308,9 +311,9 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (j == 0) T2S(4, -1);
       switch (v.obs_fmt) {
-        case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
-        case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
-        default: stream_obs<CRAFT_OBS_F32, 64, true>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
+        case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
+        case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
+        default: stream_obs<CRAFT_OBS_F32, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");             // the cleared rows before the next D
       __builtin_amdgcn_wave_barrier();

@@ -1,7 +1,7 @@
 """Compact observation staging of the tile kernel (craft_obs.h, 5x5 / 7x7 windows): each env
 stages local / pooled kind masks and the row's tail bytes instead of a u8 features() row
 (craft.py:296-330), and E reads every group of 4 features off them.  Checked against the u8-row
-staging (CRAFT_COMPACT=0 at creation) on every output of every entry point that observes, for
+staging (the default; CRAFT_COMPACT=1 at creation selects compact records) on every output of every entry point that observes, for
 every observation format, tile size and a partial last tile; and at BASELINE's size (65,536 envs,
 12x12, w = 5, one round of 64-env workgroups) against the CPU oracle."""
 import numpy as np
@@ -16,10 +16,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _pair(monkeypatch, world, n, pool):
-    a = sim_with_pool(world, n, pool)                       # compact records (the default)
-    monkeypatch.setenv("CRAFT_COMPACT", "0")
-    b = sim_with_pool(world, n, pool)                       # u8 rows
+    monkeypatch.setenv("CRAFT_COMPACT", "1")
+    a = sim_with_pool(world, n, pool)                       # compact records
     monkeypatch.delenv("CRAFT_COMPACT")
+    b = sim_with_pool(world, n, pool)                       # u8 rows (the default)
     return a, b
 
 
@@ -78,7 +78,7 @@ def test_compact_equals_u8_rows(monkeypatch, world, W, n, tile, fmt):
     b.check()
 
 
-def test_compact_full_size_vs_oracle(oracle_mod):
+def test_compact_full_size_vs_oracle(oracle_mod, monkeypatch):
     """65,536 12x12 envs with 5x5 windows (the 64-env compact tiles: 1024 workgroups, one
     round), one craft_step per tick with auto-reset: 256 random global ids against the oracle
     every tick (observation, done, success, reward) and their states at the end."""
@@ -87,7 +87,9 @@ def test_compact_full_size_vs_oracle(oracle_mod):
     pool, _, _ = sample_scenarios(params, cb, 123, 1024)
     n, T = 65536, 45
     specs = synthetic_specs(pool, 12, 12, n, 0, seed=1, task_ids=[t.id for t in tm.dataset_tasks()])
+    monkeypatch.setenv("CRAFT_COMPACT", "1")
     sim = sim_with_pool(world, n, pool)
+    monkeypatch.delenv("CRAFT_COMPACT")
     assert sim.tile_shape()[0] == 64
     sim.reset(*specs)
     gids = np.sort(np.random.RandomState(7).choice(n, 256, replace=False))

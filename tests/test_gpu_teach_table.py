@@ -1,8 +1,8 @@
 """The teacher table (craft_teach.h): find_closest_resources answered ahead of time for every
 pool row's pristine grid, read by every teacher query whose env has cleared no cell.  It is the
 same function evaluated earlier, so every label, path length and summary must equal the BFS's
-(CRAFT_TEACH_TABLE=0 at creation turns the table off; the fused tick + teacher kernels read it
-only with CRAFT_TT_FUSED=1, which these tests set).  The reference fixtures of
+(CRAFT_TEACH_TABLE=0 at creation turns the table off; CRAFT_TT_FUSED=0 keeps the fused tick +
+teacher kernels off it, which these tests set to 1, the default, explicitly).  The reference fixtures of
 tests/test_gpu_parity.py (teacher_12x12.npz with its raising calls, the 4400 demonstrations) run
 through the table path too: their states are set with set_state, i.e. pristine grids."""
 import numpy as np
@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 def _pair(monkeypatch, world, n, pool):
     out = []
-    monkeypatch.setenv("CRAFT_TT_FUSED", "1")             # the fused kernels read the table too
+    monkeypatch.setenv("CRAFT_TT_FUSED", "1")             # the fused kernels read the table (default)
     for flag in ("1", "0"):
         monkeypatch.setenv("CRAFT_TEACH_TABLE", flag)
         s = CraftSim(world, n_envs=n, device=0, pool_capacity=len(pool))

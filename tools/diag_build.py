@@ -2,7 +2,7 @@
 from the product's objects except the named translation units, which are compiled again with
 -DCRAFT_STAMPS (s_memrealtime phase stamps, craft_device.h) and any extra defines.
 
-    python tools/diag_build.py craft_sim craft_tile [-DNAME ...] [--out libname.so]"""
+    python tools/diag_build.py craft_sim craft_tile [-DNAME ...] [--out libname.so] [--no-stamps]"""
 import os
 import subprocess
 import sys
@@ -14,7 +14,7 @@ import __graft_entry__ as ge  # noqa: E402
 DIAG = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_diag.so")
 
 
-def build(stamped=("craft_sim", "craft_tile"), defines=(), out=DIAG):
+def build(stamped=("craft_sim", "craft_tile"), defines=(), out=DIAG, stamps=True):
     ge.build()
     obj = os.path.join(REPO, "psketch_amd", "lib", "obj")
     dobj = os.path.join(REPO, "psketch_amd", "lib", "obj_diag" + "".join("_" + d[2:].lower() for d in defines))
@@ -25,7 +25,7 @@ def build(stamped=("craft_sim", "craft_tile"), defines=(), out=DIAG):
         if base in stamped:
             o = os.path.join(dobj, base + ".o")
             subprocess.check_call([ge.HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                                   "-DCRAFT_STAMPS", *defines, "-c", os.path.join(ge.CSRC, src), "-o", o])
+                                   *(["-DCRAFT_STAMPS"] if stamps else []), *defines, "-c", os.path.join(ge.CSRC, src), "-o", o])
         else:
             o = os.path.join(obj, base + ".o")
         objs.append(o)
@@ -40,5 +40,7 @@ if __name__ == "__main__":
         i = args.index("--out")
         out = os.path.join(REPO, "psketch_amd", "lib", args[i + 1])
         del args[i:i + 2]
+    stamps = "--no-stamps" not in args        # an A/B variant of the product: the defines only
+    args = [a for a in args if a != "--no-stamps"]
     names = [a for a in args if not a.startswith("-D")]
-    build(tuple(names) or ("craft_sim", "craft_tile"), [a for a in args if a.startswith("-D")], out)
+    build(tuple(names) or ("craft_sim", "craft_tile"), [a for a in args if a.startswith("-D")], out, stamps)
