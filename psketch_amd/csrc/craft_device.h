@@ -55,8 +55,9 @@ struct SimView {
   // (tt_slot: 4 bits per kind id, 0xf = none); null when the table is off (too large)
   const uint16_t* ttab;
   int32_t tt_slots;
-  int32_t tt_fused;           // 1 (default): the fused tick + teacher kernels read the table too
-                              // (CRAFT_TT_FUSED=0 at creation: they defer every go[X] BFS instead)
+  int32_t tt_fused;           // 1: the fused tick + teacher kernels read the table too (set per
+                              // launch by craft_step_teach, CRAFT_TT_FUSED; 0: they defer every
+                              // go[X] BFS instead)
   uint64_t tt_slot[2];
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |

@@ -149,6 +149,10 @@ struct craft_sim {
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   uint16_t* d_ttab = nullptr;       // the teacher table (craft_teach.h), or null
+  // whether craft_step_teach's kernels read the table (CRAFT_TT_FUSED: 0 never, 1 always, 2 auto:
+  // when the launch rewrites the previous launch's observation buffer, as a trainer's loop does)
+  int tt_mode = 2;
+  const void* last_teach_obs = nullptr;
   int32_t tt_kinds[16] = {};        // its slots' target kinds
   SimView view{};
   int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
@@ -323,7 +327,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   const char* prio_env = getenv("CRAFT_T2_PRIO");
   s->view.t2_prio = prio_env ? atoi(prio_env) : 0;
   const char* ttf_env = getenv("CRAFT_TT_FUSED");
-  s->view.tt_fused = ttf_env ? (atoi(ttf_env) != 0) : 1;
+  s->tt_mode = ttf_env ? std::min(std::max(atoi(ttf_env), 0), 2) : 2;
+  s->view.tt_fused = s->tt_mode == 1;
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
@@ -700,15 +705,23 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   const int nw = craft::teach_words(s->view.W, s->view.H);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
+  // Teacher-table reads in the fused kernel: one L2 line per pristine env.  They hit the
+  // Infinity Cache when the launch rewrites the previous launch's observation buffer (a trainer's
+  // loop: ring 1, -2.5 us per tick) and go to HBM beside the store stream when every launch
+  // writes a fresh buffer (a 16-slot ring: +0.5 us), so auto mode reads them only in the first
+  // case (profiles/r04/ab5).
+  SimView v = s->view;
+  if (s->tt_mode == 2) v.tt_fused = (a.obs == nullptr || a.obs == s->last_teach_obs) ? 1 : 0;
+  s->last_teach_obs = a.obs;
   if (kernel == 2) {
-    e = craft::launch_tick2(tl, nw, s->view, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
+    e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
   } else {
     const int tile = craft::kMaxTileEnvs;
     const size_t lds = (size_t)craft::tile_lds_layout(tile, s->view.GS, s->view.F, s->view.cpt != 0,
                                                       s->cfg.window_width, s->view.K).bytes + tile * 4 +
                        CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16 + tile * 4;
     // + task | frozen words, task_sub, D sync and the deferred-BFS controls, the deferred list
-    e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, s->view, a, lds, st);
+    e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, v, a, lds, st);
   }
   if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
   return CRAFT_OK;
