@@ -48,8 +48,6 @@ struct SimView {
   int32_t bridge, axe;
   int32_t obs_policy;         // observation stores: 0 write-back, 1 nontemporal, 2 write-through (sc1)
   int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
-  int32_t cpt;                // 1: the tile kernel stages compact records (craft_obs.h), 5x5 / 7x7 windows
-  int32_t t2_prio;            // tick2 kernel wave priorities (CRAFT_T2_PRIO, an A/B knob; 0 = none)
   // The teacher's BFS answers on every pool row's pristine grid (craft_teach.h teach_table):
   // ttab[((row * tt_slots + slot) * 4 + dir) * C + cell], slot = the target kind's slot
   // (tt_slot: 4 bits per kind id, 0xf = none); null when the table is off (too large)
@@ -124,33 +122,6 @@ __host__ __device__ inline LdsLayout lds_layout(int tile, int GS, int F, int obs
   l.bytes = l.ctrl + 16;
   return l;
 }
-
-// The tile kernel's dynamic LDS.  With compact staging (cpt, 5x5 / 7x7 windows) the "obs" piece
-// holds the tile's compact records [tile][RS] words (craft_obs.h) instead of the u8 rows
-// [tile][F]: the one-hot part of a row as a bit string, then its tail as bytes -- 41 words for a
-// 5x5 row of 1076 bytes.
-__host__ __device__ inline int compact_tail_words(int K) { return (K + 5 + 3) / 4; }
-__host__ __device__ inline int compact_bit_words(int win, int K) { return (2 * win * win * K + 31) / 32; }
-__host__ __device__ inline int compact_stride(int win, int K) {
-  return (compact_bit_words(win, K) + compact_tail_words(K)) | 1;   // odd: rows spread over banks
-}
-__host__ __device__ inline int compact_obs_bytes(int tile, int win, int K, int F) {
-  (void)F;
-  return (tile * compact_stride(win, K) * 4 + 15) & ~15;
-}
-__host__ __device__ inline LdsLayout tile_lds_layout(int tile, int GS, int F, bool cpt, int win, int K) {
-  if (!cpt) return lds_layout(tile, GS, F);
-  // the same carve with the compact piece in place of the rows: lds_layout's obs size is tile * F
-  // rounded up to 16, so pass an F' that reproduces the compact piece's size exactly
-  const int ob = compact_obs_bytes(tile, win, K, F);
-  LdsLayout l = lds_layout(tile, GS, 0);
-  const int shift = (ob + 15) & ~15;
-  l.inv += shift; l.task += shift; l.rc += shift; l.agent += shift; l.ctrl += shift; l.bytes += shift;
-  return l;
-}
-// Whether a handle's tile kernels use compact staging: 5x5 / 7x7 windows and rows a whole number
-// of 4-value groups (F % 4 == 0: an fp32 row is whole 16-byte stores).
-__host__ __device__ inline bool compact_ok(int win, int K, int F) { (void)K; return win >= 5 && F % 4 == 0; }
 
 struct TileArgs {
   const int32_t* src;

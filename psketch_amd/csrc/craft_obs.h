@@ -190,191 +190,6 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
   }
 }
 
-// ---- compact staging (5x5 / 7x7 windows, the tile kernel) ------------------------------------
-// A 5x5 features() row is 1076 bytes, so 64 u8 rows (69 KB) leave room for two tile workgroups
-// per CU and 65,536 envs run in two rounds.  Instead each env stages a record of RS words:
-//   [0, NB)        the one-hot part of the row, features [0, L2 = 2*W2*K) (local, then pooled),
-//                  as a bit string: feature f is bit f % 32 of word f / 32
-//   [NB, NB + TW)  the row's tail as bytes: inventory counts [K], dir one-hot [4], the 0
-// 41 words for a 5x5 row.  A group of 4 features (one 16-byte fp32 store) below L2 is one nibble
-// of one word, so E reads one word per store and spreads the nibble into 4 bytes with a multiply;
-// only the few groups at and past L2 take the per-value path.
-struct CompactShape {
-  int L2, NB;                                   // one-hot features; bit-string words
-};
-
-__device__ __forceinline__ uint32_t compact_value(const uint32_t* rec_e, int f, CompactShape cs) {
-  if (f < cs.L2) return (rec_e[f >> 5] >> (f & 31)) & 1u;
-  const int b = f - cs.L2;
-  return (rec_e[cs.NB + (b >> 2)] >> (8 * (b & 3))) & 0xffu;
-}
-
-// Features 4q .. 4q+3 of a record, one byte each.
-__device__ __forceinline__ uint32_t compact_group(const uint32_t* rec_e, int q, CompactShape cs) {
-  if (4 * q + 3 < cs.L2) {
-    const uint32_t nib = __builtin_amdgcn_ubfe(rec_e[q >> 3], 4u * (q & 7), 4u);
-    return (nib * 0x204081u) & 0x01010101u;     // bit j -> byte j (the four partial products
-  }                                             // occupy disjoint bits: no carries)
-  uint32_t out = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) out |= compact_value(rec_e, 4 * q + j, cs) << (8 * j);
-  return out;
-}
-
-// OR a K-bit field (bits of `m`, K <= 32) into the bit string at bit p.
-__device__ __forceinline__ void or_field(uint32_t* rec, int p, uint32_t m) {
-  const int w = p >> 5, sh = p & 31;
-  atomicOr(rec + w, m << sh);
-  const uint32_t hi = sh ? (m >> (32 - sh)) : 0u;
-  if (hi) atomicOr(rec + w + 1, hi);
-}
-
-// Phase D with compact records, one env split over P lanes (as scatter_env_part): unit 0 writes
-// the tail words; unit 1 + c takes grid column c of the pooled window, block by block (blocks
-// wholly outside the grid skipped): its WIN cells' kind bits OR-ed into one mask, the mask OR-ed
-// into the block's K-bit field.  The local window is the pooled window's centre block
-// (x - hw .. x + hw, y - hw .. y + hw), so the centre column's units also set the local bits from
-// the same reads.  Lanes of an env share words (the local/pooled boundary, the columns of one
-// block), so every bit goes in with an LDS atomic OR; the bit string must be zero beforehand.
-template <int WIN, int P>
-__device__ __forceinline__ void scatter_env_compact(const SimView& v, const uint8_t* g, const uint8_t* iv,
-                                                    uint32_t ag, uint32_t* rec, int NB, int part) {
-  const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
-  const int W = v.W, H = v.H, K = v.K;
-  constexpr int W2 = WIN * WIN, hw = WIN / 2, bh = W2 / 2;
-  const int L = W2 * K;
-  const int cxa = max(x - bh, 0), cxb = min(x - bh + W2 - 1, W - 1);
-  const int nc = cxb - cxa + 1;
-#pragma unroll 1
-  for (int unit = part; unit <= nc; unit += P) {
-    if (unit == 0) {
-      // the tail: inventory bytes [0, K) (tail word t is inventory word t, its bytes past K
-      // cleared), the dir one-hot at byte K + dir, then zeros (K <= 32: at most 10 words)
-      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);
-      const int TW = compact_tail_words(K), db = K + dir;
-#pragma unroll
-      for (int t = 0; t < (CRAFT_MAX_KINDS + 5 + 3) / 4; ++t) {
-        if (t < TW) {
-          const int nb = min(max(K - 4 * t, 0), 4);                   // inventory bytes in word t
-          uint32_t o = t < 8 ? (ivw[t] & (nb == 4 ? ~0u : (1u << (8 * nb)) - 1u)) : 0u;
-          o |= ((db >> 2) == t) ? (1u << (8 * (db & 3))) : 0u;
-          rec[NB + t] = o;
-        }
-      }
-    } else {
-      const int cx = cxa + unit - 1;
-      const int bi = (cx - x + bh) / WIN;
-      const int li = cx - x + hw;                                     // local row, if in [0, WIN)
-      const uint8_t* col = g + cx * H;
-#pragma unroll
-      for (int b = 0; b < WIN; ++b) {
-        const int cy0 = y - bh + b * WIN;
-        if (cy0 >= H || cy0 + WIN <= 0) continue;                     // the block is padding
-        int kk[WIN];
-        uint32_t m = 0;
-#pragma unroll
-        for (int jj = 0; jj < WIN; ++jj) {                            // unconditional reads, masked
-          const int cy = cy0 + jj;
-          const int k = col[min(max(cy, 0), H - 1)];
-          kk[jj] = (unsigned)cy < (unsigned)H ? k : 0;
-          m |= 1u << kk[jj];
-        }
-        m &= ~1u;                                                     // kind 0 = empty
-        if (m) or_field(rec, L + (bi * WIN + b) * K, m);
-        if (b == hw && (unsigned)li < (unsigned)WIN) {                // the local window's column
-#pragma unroll
-          for (int jj = 0; jj < WIN; ++jj)
-            if (kk[jj]) {
-              const int f = ((li * WIN) + jj) * K + kk[jj];
-              atomicOr(rec + (f >> 5), 1u << (f & 31));
-            }
-        }
-      }
-    }
-  }
-}
-
-template <int WIN, int TILE, int NTHR = kThreads>
-__device__ __forceinline__ void scatter_compact(const SimView& v, const uint8_t* s_grid, const uint8_t* s_inv,
-                                                const uint32_t* s_agent, uint32_t* s_rec, int RS, int nE, int tid) {
-  constexpr int kParts = NTHR / TILE;
-  const int e = tid % TILE, part = tid / TILE;
-  const uint32_t ag = s_agent[e];
-  if (e < nE && (ag >> 24))
-    scatter_env_compact<WIN, kParts>(v, s_grid + e * v.GS, s_inv + e * kInvStride, ag, s_rec + e * RS,
-                                     compact_bit_words(WIN, v.K), part);
-}
-
-// 16 bytes of output from four packed feature-byte words (as pack16 on the u8 rows).
-template <int FMT>
-__device__ __forceinline__ obs_vec pack_bytes(const uint32_t* b) {
-  if (FMT == CRAFT_OBS_F32) {
-    const uint32_t w = b[0];
-    return obs_vec{__float_as_uint((float)(w & 0xff)), __float_as_uint((float)((w >> 8) & 0xff)),
-                   __float_as_uint((float)((w >> 16) & 0xff)), __float_as_uint((float)(w >> 24))};
-  } else if (FMT == CRAFT_OBS_BF16) {
-    auto bf = [](uint32_t x) { return __float_as_uint((float)x) >> 16; };
-    auto two = [&](uint32_t x) { return bf(x & 0xff) | (bf((x >> 8) & 0xff) << 16); };
-    return obs_vec{two(b[0]), two(b[0] >> 16), two(b[1]), two(b[1] >> 16)};
-  } else {
-    return obs_vec{b[0], b[1], b[2], b[3]};
-  }
-}
-
-// Phase E with compact records: the tile's rows as one flat stream of 16-byte stores, exactly as
-// stream_obs streams the u8 rows (consecutive lanes, consecutive 16 bytes: every wave store is
-// whole cache lines), each store's 4 / 8 / 16 values read off the records one group at a time.
-// The lane's group is tracked as (row e, group q) and advanced, never divided.
-template <int FMT, int NTHR = kThreads>
-__device__ __forceinline__ void stream_compact(const uint32_t* s_rec, void* obs, int64_t env0, int F, int RS,
-                                               CompactShape cs, int nE, int policy, int tid) {
-  constexpr int ESZ = FMT == CRAFT_OBS_F32 ? 4 : (FMT == CRAFT_OBS_BF16 ? 2 : 1);
-  constexpr int PER = 16 / ESZ;                // values per 16-byte store
-  constexpr int GPS = PER / 4;                 // groups per store
-  const int G = F >> 2;                        // groups per row
-  const int total = nE * F;
-  const int nv = total / PER;
-  uint8_t* tile_out = static_cast<uint8_t*>(obs) + env0 * (int64_t)F * ESZ;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(tile_out, 0, total * ESZ, 0x00020000);
-  constexpr int U = 4;
-  int ge = (tid * GPS) / G, gq = tid * GPS - ge * G;
-  for (int base = tid; base < nv; base += U * NTHR) {
-    obs_vec o[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int sidx = base + u * NTHR;
-      if (sidx < nv) {
-        uint32_t b[GPS];
-        int e = ge, q = gq;
-#pragma unroll
-        for (int j = 0; j < GPS; ++j) {
-          b[j] = compact_group(s_rec + e * RS, q, cs);
-          if (GPS > 1 && ++q == G) { q = 0; ++e; }
-        }
-        o[u] = pack_bytes<FMT>(b);
-      }
-      gq += NTHR * GPS;                          // the next store slot of this lane
-      while (gq >= G) { gq -= G; ++ge; }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int sidx = base + u * NTHR;
-      if (sidx < nv) {
-        if (policy == 1) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 2);         // nt
-        else if (policy == 2) __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 16);   // sc1
-        else __builtin_amdgcn_raw_buffer_store_b128(o[u], rsrc, sidx * 16, 0, 0);
-      }
-    }
-  }
-  for (int f = nv * PER + tid; f < total; f += NTHR) {       // the last few values of the tile
-    const int e = f / F, ff = f - e * F;
-    const uint32_t bt = compact_value(s_rec + e * RS, ff, cs);
-    if (FMT == CRAFT_OBS_F32) reinterpret_cast<float*>(tile_out)[f] = (float)bt;
-    else if (FMT == CRAFT_OBS_BF16) reinterpret_cast<uint16_t*>(tile_out)[f] = (uint16_t)(__float_as_uint((float)bt) >> 16);
-    else tile_out[f] = (uint8_t)bt;
-  }
-}
-
 // Phase D: all threads scatter the non-zero bytes of each env's features() row
 // into the zeroed u8 rows s_obs[TILE][F] (scatter_env_part, NTHR / TILE threads per
 // env).  s_agent[e] = x | y<<8 | dir<<16 | 1<<24 for a live env (0 = skip).

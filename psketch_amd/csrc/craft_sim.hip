@@ -193,10 +193,9 @@ int hip_fail(craft_sim* sim, hipError_t e, const char* what) {
 using craft_host::validate_config;
 
 // The tile kernel's default envs per workgroup (craft_sim_create, craft_sim_tune(0, ...)).
-int default_tile(int win, bool cpt) {
-  if (win == 3) return 64;
-  if (win == 5) return cpt ? 64 : 32;
-  return 32;                      // 7x7: 32-env u8 rows (67 KB) measured 3 % faster than 16 at 16x16
+int default_tile(int win) {
+  // 3x3: 64-env tiles; 5x5: 32 (35 KB of rows); 7x7: 32 (67 KB), 3 % faster than 16 at 16x16
+  return win == 3 ? 64 : 32;
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -214,10 +213,10 @@ size_t lds_bytes(const craft_sim* s, int tile, int obs_bufs = 1, bool pristine =
   return b;
 }
 
-// The tile kernel's (craft_tile.h): u8 rows, or compact records for 5x5 / 7x7 windows (v.cpt).
+// The tile kernel's (craft_tile.h).
 size_t tile_lds_bytes(const craft_sim* s, int tile) {
   const SimView& v = s->view;
-  size_t b = (size_t)craft::tile_lds_layout(tile, v.GS, v.F, v.cpt != 0, s->cfg.window_width, v.K).bytes;
+  size_t b = (size_t)craft::lds_layout(tile, v.GS, v.F).bytes;
   if (s->resident_cap > 0) {
     const size_t capped = ((size_t)163840 / s->resident_cap) & ~size_t(15);
     if (capped > b) b = capped;
@@ -317,15 +316,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   // stats rows: one per 16-env tile, plus the step kernel's last workgroup's tick waves (its
   // wave count is rounded up to the workgroup's 4)
   s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs + 4;
-  // default tile: 64 envs for 3x3 rows, 32 for 5x5 and 7x7 rows.  Compact records for 5x5 / 7x7
-  // windows (craft_obs.h) are an option (CRAFT_COMPACT=1 at creation: 64-env tiles for 5x5, one
-  // round of workgroups), measured slower than the u8 rows at every shape
-  const char* cpt_env = getenv("CRAFT_COMPACT");
-  s->view.cpt = craft::compact_ok(cfg->window_width, cfg->n_kinds, cfg->n_features) &&
-                (cpt_env && atoi(cpt_env) == 1) ? 1 : 0;
-  s->tile = default_tile(cfg->window_width, s->view.cpt != 0);
-  const char* prio_env = getenv("CRAFT_T2_PRIO");
-  s->view.t2_prio = prio_env ? atoi(prio_env) : 0;
+  s->tile = default_tile(cfg->window_width);
   const char* ttf_env = getenv("CRAFT_TT_FUSED");
   s->tt_mode = ttf_env ? std::min(std::max(atoi(ttf_env), 0), 2) : 2;
   s->view.tt_fused = s->tt_mode == 1;
@@ -450,7 +441,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
 int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_cu, int32_t obs_store) {
   if (!s) return CRAFT_EINVAL;
   s->tile_knob = tile_envs;
-  if (tile_envs == 0) tile_envs = default_tile(s->cfg.window_width, s->view.cpt != 0);
+  if (tile_envs == 0) tile_envs = default_tile(s->cfg.window_width);
   if (tile_envs != 16 && tile_envs != 32 && tile_envs != 64)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune: tile_envs must be 16, 32 or 64");
   if (max_resident_per_cu != 0 && (max_resident_per_cu < 3 || max_resident_per_cu > 32))
@@ -717,8 +708,7 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
     e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
   } else {
     const int tile = craft::kMaxTileEnvs;
-    const size_t lds = (size_t)craft::tile_lds_layout(tile, s->view.GS, s->view.F, s->view.cpt != 0,
-                                                      s->cfg.window_width, s->view.K).bytes + tile * 4 +
+    const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
                        CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16 + tile * 4;
     // + task | frozen words, task_sub, D sync and the deferred-BFS controls, the deferred list
     e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, v, a, lds, st);

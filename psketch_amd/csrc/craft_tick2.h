@@ -296,7 +296,6 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
 
   if (wave < kTick2Waves) {
     if (!want_obs) return;
-    if (v.t2_prio & 1) __builtin_amdgcn_s_setprio(2);   // A/B knob: the stores ahead of the BFS
     // ---- D + E per wave: envs 16w..16w+15 of each tile, rows private to the wave ---------------
     uint8_t* s_obsw = smem + lay.obs + wave * obs_w;
 #pragma unroll 1
@@ -333,7 +332,6 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   if constexpr (TL > 0) {
     // ---- T: DemonstrationTeacher on each env's new state (teachers/demonstration.py:9-30) from
     // the rows C left in LDS, TL lanes per env, overlapping D + E -----------------------------------
-    if (v.t2_prio & 2) __builtin_amdgcn_s_setprio(3);   // A/B knob: the BFS ahead of the stores
     const int u = tid - 64 * kTick2Waves;
     const int j = u / (kTick2Tile * TL), e = (u % (kTick2Tile * TL)) / TL, ql = u % TL;
     if (e < tile_envs(j)) {

@@ -32,15 +32,9 @@ namespace craft {
 template <int WIN, int MODE, int TILE, int TL = 0, int NW = 0>
 __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) void tile_kernel(SimView v, TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // compact staging (craft_obs.h) for 5x5 / 7x7 windows: bit-string records in place of the u8
-  // rows, so a 64-env tile fits 4 workgroups per CU (the host sets v.cpt, compact_ok)
-  constexpr bool kCptWin = WIN >= 5;
-  const bool cpt = kCptWin && v.cpt;
-  const LdsLayout lay = tile_lds_layout(TILE, v.GS, v.F, cpt, WIN, v.K);
-  const int RS = compact_stride(WIN, v.K);
+  const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
   uint8_t* s_grid = smem;
   uint8_t* s_obs = smem + lay.obs;
-  uint32_t* s_rec = reinterpret_cast<uint32_t*>(s_obs);
   uint8_t* s_inv = smem + lay.inv;
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
@@ -305,14 +299,10 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
       }
     }
   } else if (want_obs && tid < kThreads) {
-    // waves 1-3: zero the tile's observation bytes (compact: its records) while wave 0 runs A + C
-    if (kCptWin && cpt) {
-      for (int i = tid - TILE; i < TILE * RS; i += kThreads - TILE) s_rec[i] = 0u;
-    } else {
-      uint4* z = reinterpret_cast<uint4*>(s_obs);
-      const int n16 = (nE * F + 15) >> 4;
-      for (int i = tid - TILE; i < n16; i += kThreads - TILE) z[i] = make_uint4(0, 0, 0, 0);
-    }
+    // waves 1-3: zero the tile's observation bytes while wave 0 runs A + C
+    uint4* z = reinterpret_cast<uint4*>(s_obs);
+    const int n16 = (nE * F + 15) >> 4;
+    for (int i = tid - TILE; i < n16; i += kThreads - TILE) z[i] = make_uint4(0, 0, 0, 0);
   }
   STAMP(3);
   if (TL == 0 && !want_obs) {
@@ -323,10 +313,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
   STAMP(4);
 
   // ---- D: scatter the observation's non-zero bytes ---------------------------------------------
-  if (want_obs && tid < kThreads) {
-    if (kCptWin && cpt) scatter_compact<WIN, TILE>(v, s_grid, s_inv, s_agent, s_rec, RS, nE, tid);
-    else scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
-  }
+  if (want_obs && tid < kThreads) scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
   if (TL == 0) {
     if (want_obs) __syncthreads();
   } else if (want_obs && tid < kThreads) {
@@ -390,16 +377,6 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
   }
 
   // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
-  if (kCptWin && cpt) {
-    const CompactShape cs{2 * WIN * WIN * v.K, compact_bit_words(WIN, v.K)};
-    switch (v.obs_fmt) {
-      case CRAFT_OBS_BF16: stream_compact<CRAFT_OBS_BF16>(s_rec, a.obs, env0, F, RS, cs, nE, v.obs_policy, tid); break;
-      case CRAFT_OBS_U8: stream_compact<CRAFT_OBS_U8>(s_rec, a.obs, env0, F, RS, cs, nE, v.obs_policy, tid); break;
-      default: stream_compact<CRAFT_OBS_F32>(s_rec, a.obs, env0, F, RS, cs, nE, v.obs_policy, tid); break;
-    }
-    STAMP_END();
-    return;
-  }
   switch (v.obs_fmt) {
     case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
     case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
