@@ -1,7 +1,8 @@
 #!/bin/bash
 # Every bench line of the round on one box (no profiler attached), one JSON file each in $OUT:
 # the driver's command, 512 steps, the one-tick kernel (16-slot ring and one reused buffer),
-# config 5 (fused teacher), the closed-loop trainer, and the w = 5 rollout and one-tick lines.
+# config 5 (fused teacher), the closed-loop trainer, the w = 5 rollout and one-tick lines, and
+# config 5 at w = 5.
 set -u
 REPO="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$REPO/gpurun_out/${TAG:-lines}"
@@ -21,3 +22,4 @@ run config5 --workload teacher --steps 200 --warmup 20
 run trainer --workload trainer --steps 5 --warmup 2
 run w5 --world craft_medium_12x12_w5 --steps 20 --warmup 5
 run w5_k1 --world craft_medium_12x12_w5 --ticks-per-launch 1 --steps 100 --warmup 10
+run config5_w5 --world craft_medium_12x12_w5 --workload teacher --steps 100 --warmup 10

@@ -84,10 +84,11 @@ def main():
         sim.tune(0, 0, 2)
         if args.teacher:
             for pol in args.obs_store:
-                sim.tune(0, 0, pol)
-                for k, name in ((2, "teach_tick2"), (1, "teach_tile")):
-                    sim.tune_teach(k)
-                    res[f"{name}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
+                for tl in args.tiles:
+                    sim.tune(tl, 0, pol)
+                    for k, name in ((2, "teach_tick2"), (1, "teach_tile")):
+                        sim.tune_teach(k)
+                        res[f"{name}{tl or ''}_p{pol}_us"] = round(timeit(teach, args.iters), 2)
             sim.tune(0, 0, 2)
             sim.tune_teach(0)
         print(json.dumps(res), flush=True)
