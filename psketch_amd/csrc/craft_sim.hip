@@ -26,7 +26,7 @@ hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t
 hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
                              hipStream_t st);
 hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
-size_t tick2_lds_bytes(int tl, int GS, int F);
+size_t tick2_lds_bytes(int tl, int nw, int GS, int F);
 hipError_t launch_teach_table(int nw, const SimView& v, int32_t first, int32_t count, const int32_t* kinds,
                               hipStream_t st);
 
@@ -705,7 +705,7 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   if (s->tt_mode == 2) v.tt_fused = (a.obs == nullptr || a.obs == s->last_teach_obs) ? 1 : 0;
   s->last_teach_obs = a.obs;
   if (kernel == 2) {
-    e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, s->view.GS, s->view.F), st);
+    e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, nw, s->view.GS, s->view.F), st);
   } else {
     const int tile = craft::kMaxTileEnvs;
     const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +

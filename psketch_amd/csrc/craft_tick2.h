@@ -36,11 +36,16 @@ constexpr int kTick2Tile = 64;          // envs per tile (one lane each in A + C
 
 // LDS carve: grid rows [J*64][GS] | inventory rows [J*64][kInvStride] | agent words [J*64] |
 // teacher info words [J*64] | task table [64] u16 | task_sub [64][4] | recipe words [16][3] |
-// observation rows [TW waves][up16(64/TW*F)]
+// observation rows [nbuf waves][up16(64/TW*F)] (nbuf: the tick waves, plus the teacher waves
+// when they join D + E, tick2_share)
 struct Tick2Lds {
   int inv, agent, tinfo, task, tsub, rc, work, obs, bytes;
 };
-__host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F) {
+// Whether the teacher waves take D + E chunks once their teaching is done (rows of their own):
+// pairs (2 teacher waves per tile) and grids up to 12x12, where the rows still leave two
+// workgroups per CU.
+__host__ __device__ constexpr bool tick2_share(int TL, int NW) { return TL == 2 && NW <= 4; }
+__host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F, int nbuf) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   const int n = J * kTick2Tile;
   Tick2Lds l;
@@ -50,9 +55,9 @@ __host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F) {
   l.task = l.tinfo + n * 4;
   l.tsub = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.rc = l.tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4;
-  l.work = up16(l.rc + CRAFT_MAX_RECIPES * 12);   // deferred BFS list [n] + {count, arrivals}
-  l.obs = up16(l.work + n * 4 + 8);
-  l.bytes = l.obs + TW * up16(kTick2Tile / TW * F);
+  l.work = up16(l.rc + CRAFT_MAX_RECIPES * 12);   // deferred BFS list [n] + {count, arrivals, chunk}
+  l.obs = up16(l.work + n * 4 + 12);
+  l.bytes = l.obs + nbuf * up16(kTick2Tile / TW * F);
   return l;
 }
 
@@ -69,7 +74,9 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   static_assert(J >= 1 && J < TW, "A + C runs on the first J tick waves, the rest zero the rows");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int GS = v.GS, F = v.F;
-  const Tick2Lds lay = tick2_lds(J, TW, GS, F);
+  constexpr bool SHARE = tick2_share(TL, NW);
+  constexpr int NBUF = SHARE ? TW + J * TL : TW;                        // observation row buffers
+  const Tick2Lds lay = tick2_lds(J, TW, GS, F, NBUF);
   uint8_t* s_grid = smem;
   uint8_t* s_inv = smem + lay.inv;
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
@@ -78,7 +85,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   uint32_t* s_work = reinterpret_cast<uint32_t*>(smem + lay.work);       // deferred BFS queries
-  uint32_t* s_wctl = s_work + J * kTick2Tile;                           // {count, teacher arrivals}
+  uint32_t* s_wctl = s_work + J * kTick2Tile;                  // {count, teacher arrivals, D + E chunks}
   const int obs_w = (kTick2Sub * F + 15) & ~15;
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q) sw[q] = TL > 0 ? v.task_sub[lane + 64 * q] : 0;
     if (lane < v.n_tasks) s_task[lane] = (uint16_t)tw;
     if (lane < CRAFT_MAX_RECIPES * 3) s_rc[lane] = rw;
-    if (TL > 0 && j == 0 && lane < 2) s_wctl[lane] = 0u;                  // (before the barrier)
+    if (j == 0 && lane < 3) s_wctl[lane] = 0u;                            // (before the barrier)
     if (TL > 0) {
 #pragma unroll
       for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q)
@@ -285,30 +292,34 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     }
     if (j == 0) T2S(2, 6);
   } else if (want_obs && wave < kTick2Waves) {
-    // waves J..3: zero the observation rows of every tick wave
+    // waves J..3: zero the observation rows of every wave that streams
     uint4* z = reinterpret_cast<uint4*>(smem + lay.obs);
-    const int n16 = (kTick2Waves * obs_w) >> 4;
+    const int n16 = (NBUF * obs_w) >> 4;
     for (int i = tid - 64 * J; i < n16; i += 64 * (kTick2Waves - J)) z[i] = make_uint4(0, 0, 0, 0);
   }
   if (TL == 0 && !want_obs) return;                                      // no barrier follows
   __syncthreads();
   T2S(3, -1);
 
-  if (wave < kTick2Waves) {
-    if (!want_obs) return;
-    // ---- D + E per wave: envs 16w..16w+15 of each tile, rows private to the wave ---------------
-    uint8_t* s_obsw = smem + lay.obs + wave * obs_w;
+  // ---- D + E in chunks of 16 envs of a tile (chunk c: tile c / TW, envs (c % TW) * 16 ..),
+  // claimed in order from an LDS counter by whichever wave is free, into its own LDS rows
+  auto run_chunks = [&](uint8_t* s_obsw) {
 #pragma unroll 1
-    for (int j = 0; j < J; ++j) {
-      const int e0 = j * kTick2Tile + wave * kTick2Sub;                 // first env (workgroup index)
-      const int nEw = min(kTick2Sub, tile_envs(j) - wave * kTick2Sub);
-      if (nEw <= 0) break;                                               // later tiles are empty too
+    for (;;) {
+      uint32_t c = 0;
+      if (lane == 0) c = __hip_atomic_fetch_add(&s_wctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      c = __builtin_amdgcn_readfirstlane(c);
+      if (c >= (uint32_t)(J * kTick2Waves)) break;
+      const int j = (int)c / kTick2Waves, sl = (int)c % kTick2Waves;
+      const int e0 = j * kTick2Tile + sl * kTick2Sub;                   // first env (workgroup index)
+      const int nEw = min(kTick2Sub, tile_envs(j) - sl * kTick2Sub);
+      if (nEw <= 0) continue;
       scatter_features<WIN, kTick2Sub, 64>(v, s_grid + e0 * GS, s_inv + e0 * kInvStride, s_agent + e0,
                                            s_obsw, nEw, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (j == 0) T2S(4, -1);
+      if (c == 0) T2S(4, -1);
       switch (v.obs_fmt) {
         case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
         case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
@@ -318,6 +329,11 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+  };
+
+  if (wave < kTick2Waves) {
+    if (!want_obs) return;
+    run_chunks(smem + lay.obs + wave * obs_w);
     T2SM(5);
 #ifdef CRAFT_STAMPS
     if (tid == 0 && v.stamps) {
@@ -378,6 +394,13 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     teach_deferred_dense<NW, TL>(v, s_work, (int)nw, u, J * kTick2Tile * TL, s_grid, GS, s_agent, s_tinfo,
                                  a.label + envw, envw);
     T2SM(6);
+    if constexpr (SHARE) {
+      // done teaching: take the D + E chunks no tick wave has claimed yet
+      if (want_obs) {
+        run_chunks(smem + lay.obs + (kTick2Waves + (u >> 6)) * obs_w);
+        T2SM(5);
+      }
+    }
   }
 }
 #undef T2S

@@ -58,8 +58,11 @@ hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const Ti
 // lanes per env, 4 tick waves (8 would leave the BFS too few registers at 2 workgroups per CU).
 constexpr int kTick2Tiles = 2, kTick2TickWaves = 4;
 
-size_t tick2_lds_bytes(int /*tl*/, int GS, int F) {
-  return (size_t)tick2_lds(kTick2Tiles, kTick2TickWaves, GS, F).bytes;
+size_t tick2_lds_bytes(int tl, int nw, int GS, int F) {
+  // as launch_t2_nw rounds nw up to the instantiated NW
+  const int NW = nw <= 2 ? 2 : nw <= 4 ? 4 : nw <= 5 ? 5 : 8;
+  const int nbuf = tick2_share(tl, NW) ? kTick2TickWaves + kTick2Tiles * tl : kTick2TickWaves;
+  return (size_t)tick2_lds(kTick2Tiles, kTick2TickWaves, GS, F, nbuf).bytes;
 }
 
 template <int TL, int NW>
@@ -68,6 +71,12 @@ static hipError_t launch_t2(const SimView& v, const TileArgs& a, size_t lds, hip
   const int64_t per = (int64_t)kTick2Tiles * kTick2Tile;
   const int64_t blocks = (a.n + per - 1) / per;
   if (blocks == 0) return hipSuccess;
+  if (lds > 65536) {       // the teacher waves' own rows (tick2_share) pass 64 KiB
+    if (lds > 163840) return hipErrorInvalidValue;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tick2_kernel<3, kTick2Tiles, TW, TL, NW>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL((tick2_kernel<3, kTick2Tiles, TW, TL, NW>), dim3((unsigned)blocks),
                      dim3(64 * TW + kTick2Tiles * kTick2Tile * TL), lds, st, v, a);
   return hipGetLastError();

@@ -29,6 +29,9 @@ namespace craft {
 #ifndef CRAFT_TT_WPE
 #define CRAFT_TT_WPE 4
 #endif
+#ifndef CRAFT_TILE_U
+#define CRAFT_TILE_U 4          // 16-byte stores in flight per lane of E
+#endif
 template <int WIN, int MODE, int TILE, int TL = 0, int NW = 0>
 __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) void tile_kernel(SimView v, TileArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -378,9 +381,9 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
 
   // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
   switch (v.obs_fmt) {
-    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
-    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
-    default: stream_obs<CRAFT_OBS_F32>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, kThreads, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, kThreads, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    default: stream_obs<CRAFT_OBS_F32, kThreads, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
   }
   STAMP_END();
 }
