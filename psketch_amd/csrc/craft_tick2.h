@@ -319,7 +319,10 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (c == 0) T2S(4, -1);
+#if defined(CRAFT_STAMPS) && !defined(CRAFT_STAMPS_C) && !defined(CRAFT_STAMPS_T)
+      if (c == 0 && lane == 0 && v.stamps)                              // chunk 0's wave, any wave
+        v.stamps[8 * (int64_t)blockIdx.x + 4] = __builtin_amdgcn_s_memrealtime();
+#endif
       switch (v.obs_fmt) {
         case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
         case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, 64, true, CRAFT_T2_U>(s_obsw, a.obs, envw + e0, F, nEw, v.obs_policy, lane); break;
