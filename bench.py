@@ -14,8 +14,10 @@ one craft_step launch per tick instead.
 
 --workload teacher is configs[4]: every tick also runs the on-GPU
 DemonstrationTeacher (teachers/demonstration.py) for every env, the DAgger
-label of the next tick's state, fused into the tick's launch (craft_step_teach;
---teacher-mode separate runs craft_teacher + craft_step as two launches).
+label of the next tick's state, in the same launch: up to K ticks per
+craft_rollout_teach launch (labels into a ring beside the observations), or with
+--ticks-per-launch 1 one craft_step_teach launch per tick (--teacher-mode
+separate: craft_teacher + craft_step as two launches).
 
 Inputs (scenario pool, env states) are resident in HBM before the timed region.
 Observations stream into a ring of R = 16 device buffers (1.7 GB, 6.6x the
@@ -133,9 +135,8 @@ def parse(argv=None):
         p.error("--envs, --pool and --ring must be >= 1")
     if args.tile not in (0, 16, 32, 64):
         p.error("--tile must be 0, 16, 32 or 64")
-    if args.workload == "teacher" and args.ticks_per_launch != 1:
-        # the teacher labels each tick's state, so ticks are launched one at a time
-        args.ticks_per_launch = 1
+    if args.workload == "teacher" and args.teacher_mode == "separate":
+        args.ticks_per_launch = 1                 # craft_teacher + craft_step: one tick per launch pair
     return args
 
 
@@ -322,7 +323,7 @@ def run(args):
     rank, world_size, local_rank, dev = _init_ranks(args)
 
     teacher = args.workload == "teacher"
-    K = 1 if teacher else args.ticks_per_launch
+    K = args.ticks_per_launch
     timed_plan = plan_launches(args.steps, K)
     warm_plan = plan_launches(args.warmup, K)
     k_eff = timed_plan[0]                     # = min(K, steps): the launch the events time
@@ -366,6 +367,11 @@ def run(args):
                     sim.step(seed=args.seed, tick=tick, obs=ring[r], reward=reward[r],
                              done=done[r], success=success[r])
                 tick += 1
+        elif teacher:
+            # k ticks and every env's label per tick, one craft_rollout_teach launch
+            sim.rollout_teach(k, seed=args.seed, tick0=tick, obs=ring, reward=reward, done=done,
+                              success=success, labels=labels)
+            tick += k
         else:
             if args.obs_only:
                 sim.rollout(k, seed=args.seed, tick0=tick, obs=ring)
@@ -435,7 +441,13 @@ def run(args):
         obs_bytes = {"f32": 4, "bf16": 2, "u8": 1}[sim.obs_format]
         bps = bytes_per_env_step(sim.width, sim.height, win, F, teacher, obs_bytes)
         obs_dtype = {"f32": "fp32", "bf16": "bf16", "u8": "u8"}[sim.obs_format]
-        if K > 1:
+        if K > 1 and teacher:
+            tile = 32 if win == 3 else 16
+            nw = sim.teach_words()
+            kname = f"rollout_teach_kernel<{win}, {tile}, {nw}>"
+            shape = {"tile": tile, "rollout_threads": 512, "teacher_wave": 1,
+                     "rollout_unit_ticks": k_eff, "kernel": "rollout_teach_kernel (craft_rollout_teach)"}
+        elif K > 1:
             tile, threads, split = sim.rollout_shape()          # what the library launched
             fmt = {"f32": "0", "bf16": "1", "u8": "2"}[sim.obs_format]
             kname = (f"rollout_split_kernel<{win}, {tile}, {threads}, {fmt}, *, false>" if split
@@ -462,7 +474,9 @@ def run(args):
         if teacher:
             workload += "_" + args.teacher_mode
         traffic = pmc_traffic(args, workload, k_eff)
-        if teacher:
+        if teacher and K > 1:
+            bound = "hbm (the teacher's walk and BFS run in the interval's slack beside the stream)"
+        elif teacher:
             bound = ("latency: the tick's prologue plus the BFS beside the observation stream "
                      "(store floor of the tick's bytes at the in-situ ceiling below)")
         elif K == 1:

@@ -166,12 +166,22 @@ int craft_sim_tune(craft_sim_t* sim, int32_t tile_envs, int32_t max_resident_per
  * for 3x3 windows, else the handle's tile with 256 threads (512 for 64-env tiles). */
 int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t threads);
 
-/* Which kernel craft_step_teach launches: 0 (default) = the measured best (the two-tile
- * kernel with 2 teacher lanes per env for 3x3 windows at >= 32768 envs, else the one-tile
- * kernel with 4), 1 = the one-tile kernel, 2 = the two-tile kernel (3x3 windows and the
- * default tile only; otherwise the one-tile kernel).  Results are identical for every setting.  Replaces nothing in the
- * reference (a tuning knob, like craft_sim_tune). */
-int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel);
+/* The teacher's knobs (results are identical for every setting; a tuning knob like
+ * craft_sim_tune, replacing nothing in the reference):
+ *   kernel  which kernel craft_step_teach launches: 0 (default) = the measured best (the two-tile
+ *           kernel with 2 teacher lanes per env for 3x3 windows at >= 32768 envs, else the
+ *           one-tile kernel with 4), 1 = the one-tile kernel, 2 = the two-tile kernel (3x3
+ *           windows and the default tile only; otherwise the one-tile kernel);
+ *   lanes   teacher lanes per query: 0 (default) = each kernel's measured best; 1, 2 or 4 for
+ *           craft_teacher and the one-tile kernel, 2 or 4 for the two-tile kernel (others: 2);
+ *   table   which teachers read the teacher table (find_closest_resources answered when a pool
+ *           row is loaded, for every go/get target kind, start cell and direction: 4*W*H u16
+ *           entries per kind per pool row, allocated at craft_sim_create for pool_capacity rows
+ *           when they fit in 1 GiB), for envs that have cleared no cell: 0 (default) = auto
+ *           (craft_step_teach only when its launch rewrites the previous launch's observation
+ *           buffer, where the reads hit the Infinity Cache; every other teacher always),
+ *           1 = always, 2 = never (every query runs the BFS). */
+int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel, int32_t lanes, int32_t table);
 
 /* The kernel craft_step / craft_step_ex (teach == 0) or craft_step_teach (teach != 0) will
  * launch, resolved from the knobs above: *kernel = CRAFT_KERNEL_TILE / _TICK2, *envs =
@@ -323,6 +333,42 @@ int craft_step_teach(craft_sim_t* sim, const craft_step_args_t* args, int32_t* l
 int craft_rollout(craft_sim_t* sim, const int32_t* actions, uint64_t action_seed, int64_t tick0,
                   int32_t n_ticks, uint32_t flags, void* obs, int32_t ring, float* reward,
                   uint8_t* done, int8_t* success, void* stream);
+
+/* craft_rollout with the DemonstrationTeacher in the same launch: n_ticks ticks, and after each
+ * one DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) of every slot's new state,
+ * as n_ticks craft_step_teach calls would give, with each tick's action taken per slot from
+ *   - its label (the teacher's action for its current state): every slot when label_actions
+ *     (make_data.get_reference_actions, make_data.py:146-152: the demonstrations), or the slots
+ *     with behavior_clone[i] set (DAgger's mix, trainers/imitation.py:47-57);
+ *   - otherwise the policy: actions[k][i] (device int32[n_ticks][n_envs]) or the hashed draw.
+ * The label of a slot's state before tick0 comes from label_in (device int32[n_envs]: craft_teacher's
+ * answer, or the last labels ring slot of the previous launch); required when labels feed actions.
+ * Tick k = tick0 + k writes ring slot k % ring of each output (each may be NULL): obs
+ * [ring][n_envs][n_features] (obs format), reward / done / success as craft_rollout, labels
+ * int32 [ring][n_envs] (the label of the slot's state after the tick: -1 for a slot the tick left
+ * frozen, -2 and CRAFT_ETEACHER latched where the reference raises), action_record int32
+ * [ring][n_envs] (the action taken, -1 for a slot already done: action_seqs).  Episode statistics
+ * accumulate as for craft_step.  Ordering as craft_rollout (one stream; a captured launch uses the
+ * graph's own counter).  Replaces the per-tick loop of trainers/imitation.py:43-73 with the
+ * teacher queried every tick, and make_data.get_reference_actions. */
+typedef struct {
+  const int32_t* actions;          /* int32[n_ticks][n_envs] policy actions, or NULL: the hashed draw */
+  const uint8_t* behavior_clone;   /* uint8[n_envs] 0/1: the slot acts on its label, or NULL */
+  int32_t label_actions;           /* 1: every slot acts on its label */
+  const int32_t* label_in;         /* int32[n_envs] labels of the states before tick0 */
+  uint64_t action_seed;
+  int64_t tick0;
+  int32_t n_ticks;
+  uint32_t flags;                  /* CRAFT_STEP_AUTORESET */
+  int32_t ring;                    /* ring slots of every output (>= 1) */
+  void* obs;
+  float* reward;
+  uint8_t* done;
+  int8_t* success;
+  int32_t* labels;
+  int32_t* action_record;
+} craft_rollout_teach_args_t;
+int craft_rollout_teach(craft_sim_t* sim, const craft_rollout_teach_args_t* args, void* stream);
 
 /* Sums the episode statistics accumulated by craft_step into stats_out
  * (device int64[3] = {successes, episodes ended, env-steps}) — the scalar

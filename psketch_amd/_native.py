@@ -97,6 +97,26 @@ class craft_step_args_t(ctypes.Structure):
     ]
 
 
+class craft_rollout_teach_args_t(ctypes.Structure):
+    _fields_ = [
+        ("actions", ctypes.c_void_p),
+        ("behavior_clone", ctypes.c_void_p),
+        ("label_actions", ctypes.c_int32),
+        ("label_in", ctypes.c_void_p),
+        ("action_seed", ctypes.c_uint64),
+        ("tick0", ctypes.c_int64),
+        ("n_ticks", ctypes.c_int32),
+        ("flags", ctypes.c_uint32),
+        ("ring", ctypes.c_int32),
+        ("obs", ctypes.c_void_p),
+        ("reward", ctypes.c_void_p),
+        ("done", ctypes.c_void_p),
+        ("success", ctypes.c_void_p),
+        ("labels", ctypes.c_void_p),
+        ("action_record", ctypes.c_void_p),
+    ]
+
+
 OBS_F32, OBS_BF16, OBS_U8 = 0, 1, 2
 
 _vp = ctypes.c_void_p
@@ -120,7 +140,7 @@ SIGNATURES = {
     "craft_sim_tune": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),
-    "craft_sim_tune_teach": (_i32, [_vp, _i32]),
+    "craft_sim_tune_teach": (_i32, [_vp, _i32, _i32, _i32]),
     "craft_sim_step_shape": (_i32, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                     ctypes.POINTER(_i32)]),
     "craft_sim_rollout_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
@@ -134,6 +154,7 @@ SIGNATURES = {
     "craft_step_ex": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp]),
     "craft_step_teach": (_i32, [_vp, ctypes.POINTER(craft_step_args_t), _vp, _vp]),
     "craft_rollout": (_i32, [_vp, _vp, _u64, _i64, _i32, _u32, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "craft_rollout_teach": (_i32, [_vp, ctypes.POINTER(craft_rollout_teach_args_t), _vp]),
     "craft_stats": (_i32, [_vp, _vp, _i32, _vp]),
     "craft_transition": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "craft_observe": (_i32, [_vp, _vp, _i64, _vp, _vp, _vp, _vp]),

@@ -123,6 +123,7 @@ struct craft_sim {
   std::atomic<int64_t> err_slot{-1};
   int obs_fmt = CRAFT_OBS_F32;
   int tile = 64, obs_store = 2, resident_cap = 0, rollout_chunk = 0, rollout_threads = 0, teach_kernel = 0;
+  int teach_lanes = 0, teach_table = 0;
   int threads = 1;
   std::string last_error;
 };
@@ -693,11 +694,17 @@ int craft_sim_tune_rollout(craft_sim_t* s, int32_t chunk_ticks, int32_t threads)
   return CRAFT_OK;
 }
 
-int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel) {
+int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel, int32_t lanes, int32_t table) {
   if (!s) return CRAFT_EINVAL;
   if (kernel < 0 || kernel > 2)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile) or 2 (two-tile)");
+  if (lanes != 0 && lanes != 1 && lanes != 2 && lanes != 4)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: lanes must be 0 (default), 1, 2 or 4");
+  if (table < 0 || table > 2)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: table must be 0 (auto), 1 (always) or 2 (never)");
   s->teach_kernel = kernel;
+  s->teach_lanes = lanes;
+  s->teach_table = table;      // (this variant keeps no table: every query runs the BFS)
   return CRAFT_OK;
 }
 
@@ -944,6 +951,50 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
     in.done = done ? done + r * n : nullptr;
     in.sat = success ? success + r * n : nullptr;
     run_ticks(s, in, nullptr);
+  }
+  return CRAFT_OK;
+}
+
+// craft_rollout_teach: tick by tick, the labels of each tick's new states carried to the next
+// tick's label-source slots (make_data.get_reference_actions, imitation.py:47-57)
+int craft_rollout_teach(craft_sim_t* s, const craft_rollout_teach_args_t* x, void* /*stream*/) {
+  if (!s || !x) return CRAFT_EINVAL;
+  if (x->n_ticks < 0 || x->ring < 1 || x->tick0 < 0)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: need n_ticks >= 0, ring >= 1, tick0 >= 0");
+  if (4 * s->C > 1000)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
+  const bool lsync = x->label_actions != 0 || x->behavior_clone != nullptr;
+  if (lsync && !x->label_in)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: label_actions / behavior_clone need label_in");
+  const int esz = esize(s->obs_fmt);
+  if (x->obs && ((reinterpret_cast<uintptr_t>(x->obs) & 15u) ||
+                 (x->ring > 1 && (s->n_envs * (int64_t)s->F * esz) % 16 != 0)))
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: every obs ring slot must be 16-byte aligned");
+  const int64_t n = s->n_envs;
+  std::vector<int32_t> cur(n, 0), lab(n, 0);
+  std::vector<uint8_t> src(n, 0);                    // 1: the slot acts on its label
+  for (int64_t i = 0; i < n; ++i) {
+    src[i] = x->label_actions ? 1 : (x->behavior_clone && x->behavior_clone[i] ? 1 : 0);
+    if (lsync) cur[i] = x->label_in[i];
+  }
+  for (int32_t k = 0; k < x->n_ticks; ++k) {
+    const int64_t r = (x->tick0 + k) % x->ring;
+    TickIn in{};
+    in.actions = x->actions ? x->actions + (int64_t)k * n : nullptr;
+    in.ref = cur.data();
+    in.bc = lsync ? src.data() : nullptr;
+    in.seed = x->action_seed;
+    in.tick = x->tick0 + k;
+    in.flags = x->flags;
+    in.obs = x->obs ? static_cast<uint8_t*>(x->obs) + r * n * s->F * esz : nullptr;
+    in.reward = x->reward ? x->reward + r * n : nullptr;
+    in.done = x->done ? x->done + r * n : nullptr;
+    in.sat = x->success ? x->success + r * n : nullptr;
+    in.rec = x->action_record ? x->action_record + r * n : nullptr;
+    in.label = lab.data();
+    run_ticks(s, in, nullptr);
+    if (x->labels) std::memcpy(x->labels + r * n, lab.data(), sizeof(int32_t) * n);
+    cur.swap(lab);
   }
   return CRAFT_OK;
 }

@@ -48,11 +48,15 @@ struct SimView {
   int32_t bridge, axe;
   int32_t obs_policy;         // observation stores: 0 write-back, 1 nontemporal, 2 write-through (sc1)
   int32_t obs_fmt;            // craft_obs_format_t: 0 fp32, 1 bf16, 2 u8
-  // The teacher's BFS answers on every pool row's pristine grid (craft_teach.h teach_table):
-  // ttab[((row * tt_slots + slot) * 4 + dir) * C + cell], slot = the target kind's slot
-  // (tt_slot: 4 bits per kind id, 0xf = none); null when the table is off (too large)
+  // The teacher's BFS answers (craft_teach.h teacher table) for every pool row's grid with any
+  // subset of its first tt_m clearable cells cleared:
+  //   ttab[((trow * tt_slots + slot) * 4 + dir) * C + cell],  trow = row * tt_nsub + subset,
+  // slot = the target kind's slot (tt_slot: 4 bits per kind id, 0xf = none), subset bit j = the
+  // row's clearable cell tt_cells[row] byte j cleared (0xff = no such cell); null when off
   const uint16_t* ttab;
+  const uint32_t* tt_cells;   // [P][2]: each row's first tt_m clearable cells, a byte each
   int32_t tt_slots;
+  int32_t tt_nsub;            // 1 << tt_m
   int32_t tt_fused;           // 1: the fused tick + teacher kernels read the table too (set per
                               // launch by craft_step_teach, CRAFT_TT_FUSED; 0: they defer every
                               // go[X] BFS instead)
@@ -101,6 +105,24 @@ struct SimView {
 #define STAMP_END() do {} while (0)
 #define STAMP_MAX(k) do {} while (0)
 #endif
+
+// Raises a kernel's dynamic-LDS limit past the default 64 KiB (gfx950 allows 160 KiB per
+// workgroup) once per kernel and size, not per launch: a host runtime call per launch costs every
+// tick of a trainer's loop, and a launch captured into a HIP graph is replayed without this code.
+template <auto KERNEL>
+inline hipError_t ensure_lds(size_t lds) {
+  static size_t granted = 65536;
+  if (lds <= granted) return hipSuccess;
+  if (lds > 163840) return hipErrorInvalidValue;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(KERNEL),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) granted = lds;
+  return e;
+}
+
+// envs per tile of the teacher-labelled K-tick rollout (craft_rollout_teach.h rt_tile): 32 for
+// 3x3 windows, 16 for wider ones
+__host__ __device__ constexpr int rt_tile_of(int win) { return win == 3 ? 32 : 16; }
 
 // 32-bit words per cell set of the teacher's BFS (craft_teach.h: the band of grid columns
 // 1 .. W-2, the border columns left out); the kernels' NW template argument.
@@ -169,6 +191,14 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   int64_t* grid_out;       // host side only: the launch reports its grid size here
   uint32_t* tile_done;     // per tile: chunks completed in this launch, zeroed before the launch
   int32_t flat;            // split kernel, one unit per tile: one continuous pipeline (no queue)
+  // craft_rollout_teach (craft_rollout_teach.h)
+  const int32_t* label_in; // [n_envs] the teacher's label of each slot's state before tick0
+  const uint8_t* bc;       // [n_envs] behaviour cloning: the slot acts on its label, or null
+  int32_t label_actions;   // 1: every slot acts on its label (make_data.get_reference_actions)
+  int32_t lsync;           // labels feed some slot's actions (label_actions or bc)
+  int32_t use_table;       // the teacher reads the teacher table for pristine grids
+  int32_t* labels;         // [ring][n_envs] the label of every slot's new state, or null
+  int32_t* rec;            // [ring][n_envs] the action taken (-1: none), or null
 };
 
 struct ScenarioArgs {      // craft_pool_generate

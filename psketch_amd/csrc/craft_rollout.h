@@ -462,9 +462,8 @@ static hipError_t launch_rollout_one(const SimView& v, const RolloutArgs& a, siz
   const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
   if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
   constexpr int WPE = WIN == 3 ? 4 : 2;
-  if (lds > 65536) {       // double-buffered rows past 64 KiB (gfx950 allows 160 KiB per workgroup)
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {                        // double-buffered rows past 64 KiB
+    const hipError_t e = ensure_lds<&rollout_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>>(lds);
     if (e != hipSuccess) return e;
   }
   // persistent workgroups: what the chip holds at once (occupancy of this kernel at this LDS
@@ -504,9 +503,9 @@ static hipError_t launch_rollout_split_one(const SimView& v, const RolloutArgs& 
   const size_t lds = (size_t)split_lds_bytes(TILE, v.GS, v.F, v.CS, flat);
   auto kern = flat ? rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, kFlatShape>
                    : rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>;
-  if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  {
+    const hipError_t e = flat ? ensure_lds<&rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, kFlatShape>>(lds)
+                              : ensure_lds<&rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>>(lds);
     if (e != hipSuccess) return e;
   }
   static int resident_of[2] = {0, 0};                 // per instantiation (flat or not)

@@ -1,0 +1,1029 @@
+// craft_rollout_teach.h — K rollout ticks in one launch with the DemonstrationTeacher's label of
+// every env's new state every tick (craft_rollout_teach): config 5's DAgger labels
+// (trainers/imitation.py:43-57) and make_data.get_reference_actions' demonstrations
+// (make_data.py:146-152, the actions ARE the labels), without a launch per tick.
+//
+// One launch per tick (craft_step_teach) pays the tick's prologue every tick: the loads, the
+// transition and the scatter run on every workgroup before the first observation byte leaves
+// (~7 us of ~29 at 65,536 envs).  Here a persistent workgroup keeps a tile of envs on
+// chip for all K ticks, as the split rollout kernel does (craft_rollout_split.h), with one more
+// wave for the teacher.  512 threads, one barrier per interval; interval i of a tile runs
+//   wave 0       C(i+1): the transitions (one lane per env) into grid / inventory buffer (i+1) & 1;
+//   wave 1       D(i):   the observation scatter of item i from buffer i & 1;
+//   waves 2..6   E(i-1): the observation stream of the item before, to HBM; wave 2 also stores the
+//                        teacher's finished label rows, in item order;
+//   wave 7       T(i):   the teacher on item i's post-step rows (buffer i & 1, which C(i+2)
+//                        overwrites one interval later).
+//
+// The teacher wave.  Its walk (find_incomplete_subtask, one lane per env) must finish inside the
+// interval, but a BFS chain (~30 dependent levels) is longer than an interval (~4 us), so the
+// BFS is decoupled from the item:
+//   * a go[X] leaf on a pristine grid (no cell cleared this episode) issues the teacher table's
+//     answer load (craft_teach.h teach table) and decodes it one interval later (policy actions)
+//     or right away (label actions);
+//   * any other go[X] leaf becomes a BFS job: the leaf lane builds the band bitsets of its grid
+//     row while the row is still current and queues them in LDS;
+//   * between its own duties the wave runs the queued jobs, one BFS level per step on 16 quads
+//     (lane q of a quad: the states entered by action q, as bfs_closest<NW, 4>), each quad a
+//     small state machine (forward, reachability flood, backward), taking a new job as soon as
+//     its last one ends.  Before every barrier it steps until all other waves have arrived (an
+//     LDS arrival counter), so the BFS fills the interval's slack and never holds the barrier
+//     for more than one level.
+// Labels go into LDS label rows (item g -> row g & 7, with a count of labels still pending); the
+// teacher wave issues no global store at all (a store would make its next table load wait:
+// vmcnt counts loads and stores in issue order).  Wave 2 stores each row once complete, strictly
+// in item order (ring slots may repeat within a launch), and keeps storing while it waits for the
+// teacher at each barrier, so a teacher waiting for a free row always gets one.
+//
+// Action sources, per env: the policy (the hashed draw or given actions) or the label of the
+// env's current state (label_actions: every env, make_data's demonstrations; behavior_clone[i]:
+// DAgger's mix, imitation.py:56-57).  When labels feed actions, C(i+1) waits for item i's labels,
+// and the teacher completes each item inside its interval.
+//
+// Results are identical to n_ticks craft_step_teach calls with the same action sources (tests:
+// tests/test_gpu_rollout_teach.py, tick by tick at 65,536 envs and against the oracle).
+#pragma once
+#include "craft_obs.h"
+#include "craft_teach.h"
+
+namespace craft {
+
+constexpr int kRtThreads = 512;        // C, D, 5 streaming waves, the teacher
+constexpr int kRtRows = 8;             // label rows in flight: item g -> row g & 7
+constexpr int kRtQueue = 32;           // BFS jobs waiting for a quad
+// label row control word: 0 free; kRowFill | pending labels while the teacher fills it (== kRowFill:
+// complete); kRowStoring while wave 2 copies it out
+constexpr uint32_t kRowFill = 1u << 30, kRowStoring = 1u << 29;
+// Every wait in the kernel is bounded (a few hundred ms): past the bound CRAFT_EINVARIANT latches
+// and the wave stops waiting, so a broken invariant can never hang the GPU.
+constexpr uint32_t kRtSpinCap = 1u << 22;
+
+// LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation rows [2][up16(TILE*F)] |
+// inventory rows [2][TILE][36] | agent words [2][TILE] | teacher info words [2][TILE] | task table
+// [64] u16 | subtasks [64][4] | recipe words [16][3] | control words [8] | label rows
+// [8][4 + TILE] | BFS job queue [32][2 NW + 1] | table requests [2][TILE] | clearable cells [TILE][2]
+struct RtLds {
+  int pristine, obs, inv, agent, tinfo, task, tsub, rc, ctrl, rows, jobs, treq, tcell, bytes;
+};
+__host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
+  auto up16 = [](int x) { return (x + 15) & ~15; };
+  RtLds l;
+  l.pristine = 2 * tile * GS;
+  l.obs = up16(3 * tile * GS);
+  l.inv = l.obs + 2 * up16(tile * F);
+  l.agent = up16(l.inv + 2 * tile * kInvStride);
+  l.tinfo = l.agent + 2 * tile * 4;
+  l.task = l.tinfo + 2 * tile * 4;
+  l.tsub = up16(l.task + CRAFT_MAX_TASKS * 2);
+  l.rc = l.tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4;
+  l.ctrl = l.rc + CRAFT_MAX_RECIPES * 12;
+  l.rows = up16(l.ctrl + 32);
+  l.jobs = up16(l.rows + kRtRows * (4 + tile) * 4);
+  l.treq = up16(l.jobs + kRtQueue * (2 * NW + 1) * 4);   // [2][tile] table-entry requests
+  l.tcell = l.treq + 2 * tile * 4;                         // [tile][2] each env's listed clearable cells
+  l.bytes = up16(l.tcell + tile * 8);
+  return l;
+}
+// envs per tile: 32 for 3x3 windows (as the split rollout kernel), 16 for wider ones (their
+// observation rows: 2 x 34 KB at 5x5)
+__host__ __device__ constexpr int rt_tile(int win) { return rt_tile_of(win); }
+
+// The barriers of a unit (one tile, all ticks): the claim, C(0) done, one per interval, the end.
+enum { kBClaim = 0, kBC0 = 1, kBTick = 2, kBEnd = 3 };
+
+// ---- the teacher wave's BFS: bfs_closest<NW, 4>'s passes as a per-quad state machine ----------
+enum { kQIdle = 0, kQFwd = 1, kQReach = 2, kQBwd = 3 };
+
+// (Only what cannot be recomputed cheaply stays live: the blocked masks and facing sets are
+// rebuilt from fr / tgt per level, the start and direction come from the job word.)
+template <int NW>
+struct QuadBfs {
+  int ph = kQIdle;
+  int L = -1, chosen = -1, k = 0;
+  uint32_t meta = 0;                   // the job's meta word (row, env, start, dir, conn)
+  Bits<NW> fr, tgt, V, U, claimed;
+};
+
+// Where a bounded wait gave up, for the latched error's slot field (CRAFT_EINVARIANT): bits 60-63
+// the wait (1 C's label wait, 2 the stores wave's barrier, 3 its last rows, 4 the teacher idle,
+// 5 its BFS), 32-59 the item, 0-31 a state word.
+__device__ __forceinline__ int64_t rt_where(uint32_t wait, uint32_t item, uint32_t state) {
+  return (int64_t)(((uint64_t)wait << 60) | ((uint64_t)(item & 0xfffffffu) << 32) | state);
+}
+
+// Job meta word: band start cell p0 (bits 0-7), dir (8-9), connected (10), label row (11-13),
+// env in the tile (14-19).
+__device__ __forceinline__ uint32_t rt_job_meta(int p0, int d0, int conn, int row, int env) {
+  return (uint32_t)p0 | ((uint32_t)d0 << 8) | ((uint32_t)conn << 10) | ((uint32_t)row << 11) |
+         ((uint32_t)env << 14);
+}
+
+template <int WIN, int TILE, int NW>
+__global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v, RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int NT = kRtThreads, NWAVE = NT / 64, TW = NWAVE - 1;   // the teacher is the last wave
+  constexpr int NE = NT - 192;                                        // streaming threads (waves 2..6)
+  constexpr int P = 64 / TILE;                                        // scatter lanes per env
+  constexpr int RW = 4 + TILE;                                        // label row words
+  constexpr int JW = 2 * NW + 1;                                      // job words
+  static_assert(TILE <= 32 && 64 % TILE == 0, "the teacher's walk: one lane per env");
+  auto up16 = [](int x) { return (x + 15) & ~15; };
+  const int GS = v.GS, F = v.F, H = v.H, C = v.C;
+  const RtLds lay = rt_lds(TILE, GS, F, NW);
+  // the recipe words in a VGPR (lane w: word w), loaded while every lane is active (v_readlane)
+  const uint32_t rcv = v.rcw[min((int)(threadIdx.x & 63), CRAFT_MAX_RECIPES * 3 - 1)];
+  uint8_t* s_grid = smem;                                             // [2][TILE][GS] by item parity
+  uint8_t* s_pristine = smem + lay.pristine;                          // [TILE][GS]
+  const int obs_buf = up16(TILE * F);
+  uint8_t* s_obs = smem + lay.obs;                                    // [2][obs_buf]
+  uint8_t* s_inv = smem + lay.inv;                                    // [2][TILE][kInvStride]
+  // [2][TILE] x | y<<8 | dir<<16 | live<<24 | frozen<<25 | cells cleared this episode (63 = more) << 26
+  uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
+  uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.tinfo);  // [2][TILE] task|conn<<8|scen<<10
+  uint32_t* s_treq = reinterpret_cast<uint32_t*>(smem + lay.treq);    // [2][TILE] ttab index, ~0 = none
+  uint32_t* s_tcell = reinterpret_cast<uint32_t*>(smem + lay.tcell);  // [TILE][2] tt_cells of the env's row
+  uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
+  int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
+  uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
+  // [0] the claimed unit, [1] barrier arrivals, [2] items whose labels are complete (label actions),
+  // [3] 1 + the first slot whose table answer raised, [4] its status, [5 + p] the label row of the
+  // table requests of item parity p (~0: none)
+  uint32_t* s_ctrl = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
+  uint32_t* s_rows = reinterpret_cast<uint32_t*>(smem + lay.rows);    // [8][RW]: ctrl, tag = g + 1, tile, ring slot, labels
+  uint32_t* s_jobs = reinterpret_cast<uint32_t*>(smem + lay.jobs);    // [32][JW]
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t n = v.n_envs;
+  const bool want_obs = a.obs != nullptr;
+  const bool lsync = a.lsync != 0;                                    // labels feed some env's actions
+  const int n_tiles = (int)((n + TILE - 1) / TILE);
+  const uint32_t n_units = (uint32_t)n_tiles;                          // one unit per tile: all K ticks
+
+  // ---- once per workgroup: tables, zeroed observation rows, control words ---------------------
+  for (int t = tid; t < CRAFT_MAX_TASKS; t += NT) s_task[t] = t < v.n_tasks ? v.task_tab[t] : 0;
+  for (int t = tid; t < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS; t += NT)
+    s_tsub[t] = t < v.n_tasks * CRAFT_MAX_SUBTASKS ? v.task_sub[t] : 0;
+  for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += NT) s_rc[t] = v.rcw[t];
+  {
+    uint4* z = reinterpret_cast<uint4*>(s_obs);
+    for (int i = tid; i < (2 * obs_buf >> 4); i += NT) z[i] = make_uint4(0, 0, 0, 0);
+  }
+  if (tid < 8) s_ctrl[tid] = 0u;
+  for (int i = tid; i < kRtRows * RW; i += NT) s_rows[i] = 0u;
+  __syncthreads();                                                    // (not counted: nb starts at 0)
+
+  // Barriers.  Every wave adds one arrival per barrier before s_barrier; the teacher wave first
+  // runs BFS steps until every other wave has arrived; wave 2 stores label rows until the teacher
+  // has.  (A plain s_barrier behind the wave's own LDS accesses: nothing else is handed over.)
+  uint32_t nb = 0;                                                    // barriers passed
+  auto arrive = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(&s_ctrl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto arrivals = [&]() __attribute__((always_inline)) -> uint32_t {
+    return __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&s_ctrl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  };
+  auto hw_barrier = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    ++nb;
+  };
+
+  uint32_t n_succ = 0, n_end = 0, n_step = 0;                        // wave 0's episode sums
+
+  if (wave == 0) {
+    // =============================== C: the transitions ========================================
+    Agent s{};
+    uint64_t st = 0;
+    uint32_t init_word = 0, task_word = 0, conn = 0;
+    uint32_t clr = 0, clr_prev = 0, chg = 0;
+    constexpr uint32_t kRestart = 0x80000000u;
+    int sync = 0, lab0 = 0;
+    int ncl = 0;                                                       // cells cleared this episode
+    bool live = false, lsrc = false;
+    int64_t slot = 0;
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(s_pristine + lane * GS);
+    const uint8_t* pr = s_pristine + lane * GS;
+    auto grid_of = [&](int p) __attribute__((always_inline)) { return s_grid + (p & 1) * TILE * GS + lane * GS; };
+    auto inv_of = [&](int p) __attribute__((always_inline)) { return s_inv + (p & 1) * TILE * kInvStride + lane * kInvStride; };
+    auto restore = [&](uint8_t* g, uint32_t cl) __attribute__((always_inline)) {
+      if (cl >> 31) {
+        uint32_t* gw = reinterpret_cast<uint32_t*>(g);
+        for (int q0 = 0; q0 < (v.CS >> 2); q0 += 12) {
+          uint32_t w[12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) w[j] = q0 + j < (v.CS >> 2) ? pw[q0 + j] : 0u;
+#pragma unroll
+          for (int j = 0; j < 12; ++j)
+            if (q0 + j < (v.CS >> 2)) gw[q0 + j] = w[j];
+        }
+      } else {
+        const int nc = (cl >> 24) & 3;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (i < nc) {
+            const int c = (cl >> (8 * i)) & 0xff;
+            g[c] = pr[c];
+          }
+      }
+    };
+    // ---- A: take over tile t into buffer 0 ----
+    auto load_tile = [&](int t) __attribute__((always_inline)) {
+      const int64_t env0 = (int64_t)t * TILE;
+      const int nE = (int)min((int64_t)TILE, n - env0);
+      slot = env0 + lane;
+      live = lane < nE;
+      lsrc = false;
+      uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      uint32_t ivr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (live) {
+        st = v.state[slot];
+        init_word = v.init[slot];
+        const uint4 i0 = v.inv[2 * slot], i1 = v.inv[2 * slot + 1];
+        const uint4 m0 = v.mask[2 * slot], m1 = v.mask[2 * slot + 1];
+        uint32_t bcw = 0;
+        if (a.bc) bcw = a.bc[slot];
+        if (lsync) lab0 = a.label_in[slot];
+        ivr[0] = i0.x; ivr[1] = i0.y; ivr[2] = i0.z; ivr[3] = i0.w;
+        ivr[4] = i1.x; ivr[5] = i1.y; ivr[6] = i1.z; ivr[7] = i1.w;
+        m[0] = m0.x; m[1] = m0.y; m[2] = m0.z; m[3] = m0.w;
+        m[4] = m1.x; m[5] = m1.y; m[6] = m1.z; m[7] = m1.w;
+        lsrc = a.label_actions || (bcw & 0xffu);
+        s = unpack_state(st);
+        if (s.x < 1 || s.x > v.W - 2 || s.y < 1 || s.y > v.H - 2 || s.scen >= v.pool_count) {
+          latch_error(v.err, CRAFT_EINVAL, slot);
+          live = false;
+        }
+      }
+      chg = 0;
+      clr = 0;
+      clr_prev = 0;
+      sync = 0;
+      if (live) {
+        task_word = s_task[s.task];
+        conn = v.pool_conn[s.scen];
+        if (v.ttab) {                                                  // the row's clearable cells the table lists
+          s_tcell[2 * lane] = v.tt_cells[2 * (size_t)s.scen];
+          s_tcell[2 * lane + 1] = v.tt_cells[2 * (size_t)s.scen + 1];
+        }
+        ncl = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) ncl += __popc(m[w]);
+        uint32_t* g0 = reinterpret_cast<uint32_t*>(grid_of(0));
+        uint32_t* pwm = reinterpret_cast<uint32_t*>(s_pristine + lane * GS);
+        const uint4* gsrc = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
+        const int nchunk = v.CS >> 4;
+        for (int q0 = 0; q0 < nchunk; q0 += 4) {
+          uint4 cq[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (q0 + j < nchunk) cq[j] = gsrc[q0 + j];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (q0 + j < nchunk) {
+              const int q = 4 * (q0 + j);
+              pwm[q + 0] = g0[q + 0] = cq[j].x;
+              pwm[q + 1] = g0[q + 1] = cq[j].y;
+              pwm[q + 2] = g0[q + 2] = cq[j].z;
+              pwm[q + 3] = g0[q + 3] = cq[j].w;
+            }
+        }
+        uint32_t* iv0 = reinterpret_cast<uint32_t*>(inv_of(0));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) iv0[i] = ivr[i];
+        uint8_t* b0 = grid_of(0);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {                                  // cells cleared this episode
+          uint32_t mm = m[w];
+          while (mm) {
+            const int cc = w * 32 + __ffs(mm) - 1;
+            b0[cc] = 0;
+            const uint32_t nc = (clr >> 24) & 3;
+            clr = (clr >> 31) ? clr
+                : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)cc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
+            mm &= mm - 1;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // ---- C: tick k (item g) into buffer k & 1 (trainers/imitation.py:43-73) ----
+    auto tick_c = [&](int k, uint32_t g) __attribute__((always_inline)) {
+      const int64_t tick = a.tick0 + k;
+      const int64_t r = tick % a.ring;
+      int d = 0, succ = -1, counted = 0, act = 0;
+      uint8_t* gr = grid_of(k);
+      uint8_t* iv = inv_of(k);
+      // the label of this env's current state: label_in (the unit's first tick) or the teacher's
+      // row of item g - 1, once complete (the teacher finishes each item inside its interval)
+      if (k > 0 && __ballot(live && lsrc)) {
+        for (uint32_t spins = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                     &s_ctrl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < g;) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kRtSpinCap) { latch_error(v.err, CRAFT_EINVARIANT, rt_where(1, g, 0)); break; }   // never hang
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+      s = unpack_state(st);
+      if (live) {
+        if (sync == 1) {                                               // bring the buffer up to date
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(grid_of(k + 1));
+          uint32_t* gw = reinterpret_cast<uint32_t*>(gr);
+          for (int q0 = 0; q0 < (v.CS >> 2); q0 += 12) {
+            uint32_t w[12];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) w[j] = q0 + j < (v.CS >> 2) ? src[q0 + j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 12; ++j)
+              if (q0 + j < (v.CS >> 2)) gw[q0 + j] = w[j];
+          }
+        } else if (sync == 2) {
+          if (chg == kRestart) restore(gr, clr_prev);
+          else if (chg) gr[chg - 1] = 0;
+        }
+        if (sync) {
+          const uint32_t* src = reinterpret_cast<const uint32_t*>(inv_of(k + 1));
+          uint32_t w[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) w[i] = src[i];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(iv)[i] = w[i];
+        }
+        sync = sync ? 2 : 1;
+        chg = 0;
+        if (a.actions) {
+          act = a.actions[(int64_t)k * n + slot];
+        } else {
+          const uint64_t gid = (uint64_t)(v.env_base + slot);
+          act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)tick) >> 32) % 6u);
+        }
+        if (lsrc) act = k == 0 ? lab0 : (int)s_rows[((g - 1) & (kRtRows - 1)) * RW + 4 + lane];
+        bool restart = false;
+        if (s.frozen) {
+          d = 1;
+        } else {
+          counted = 1;
+          s.timer -= 1;
+          d = (act == CRAFT_STOP) || s.timer <= 0;
+          restart = d && (a.flags & CRAFT_STEP_AUTORESET);
+        }
+        if (d) {                                                       // satisfies() of the pre-step state
+          const int goal = task_word & 0xf, arg = (task_word >> 4) & 0xff;
+          const int fc = (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir));
+          if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) succ = iv[arg] > 0;
+          else if (goal == CRAFT_GOAL_GO) succ = (int)gr[fc] == arg;
+          else succ = -1;
+        }
+        if (restart) {                                                 // CraftScenario.init, craft.py:268-273
+          s.x = init_word & 0xff; s.y = (init_word >> 8) & 0xff; s.dir = (init_word >> 16) & 3;
+          s.timer = v.maxT;
+#pragma unroll
+          for (int w = 0; w < 8; ++w) reinterpret_cast<uint32_t*>(iv)[w] = 0u;
+          restore(gr, clr);
+          clr_prev = clr;
+          clr = 0;
+          chg = kRestart;
+          ncl = 0;
+        } else if (d && !s.frozen) {
+          s.frozen = 1;
+          s.timer = max(s.timer, 0);
+        }
+        if (!d) {
+          bool inv_changed = false, mask_changed = false;
+          uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          const int fc = (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir));   // what USE clears
+          if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
+          else transition<true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv);
+          if (mask_changed) {
+            ++ncl;
+            chg = 1u + (uint32_t)fc;
+            const uint32_t nc = (clr >> 24) & 3;
+            clr = (clr >> 31) ? clr
+                : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)fc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
+          }
+        }
+        st = pack_state(s);
+        const int64_t o = r * n + slot;
+        if (a.done) a.done[o] = (uint8_t)d;
+        if (a.sat) a.sat[o] = (int8_t)succ;
+        if (a.reward) a.reward[o] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+        if (a.rec) a.rec[o] = counted ? act : -1;                     // action_seqs, imitation.py:59-61
+      }
+      const uint64_t bs = __ballot(live && counted && d && succ == 1);
+      const uint64_t be = __ballot(live && counted && d);
+      const uint64_t bt = __ballot(live && counted);
+      n_succ += (uint32_t)__popcll(bs);
+      n_end += (uint32_t)__popcll(be);
+      n_step += (uint32_t)__popcll(bt);
+      if (lane < TILE) {
+        s_agent[(k & 1) * TILE + lane] =
+            live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24) |
+                    ((uint32_t)s.frozen << 25) | ((uint32_t)min(ncl, 63) << 26))
+                 : 0u;
+        s_tinfo[(k & 1) * TILE + lane] = (uint32_t)s.task | (conn << 8) | ((uint32_t)s.scen << 10);
+      }
+    };
+    // ---- the tile's state back to HBM from buffer p (the mask rebuilt from the rows) ----
+    auto publish = [&](int p) __attribute__((always_inline)) {
+      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(inv_of(p));
+      const uint32_t* gw = reinterpret_cast<const uint32_t*>(grid_of(p));
+      uint32_t m[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m[i] = 0u;
+#pragma unroll
+      for (int q = 0; q < CRAFT_MAX_CELLS / 4; ++q)
+        if (q < (C + 3) >> 2) m[q >> 3] |= byte_tops(nonzero_bytes(pw[q]) & zero_bytes(gw[q])) << (4 * (q & 7));
+      v.state[slot] = st;
+      v.inv[2 * slot] = make_uint4(ivw[0], ivw[1], ivw[2], ivw[3]);
+      v.inv[2 * slot + 1] = make_uint4(ivw[4], ivw[5], ivw[6], ivw[7]);
+      v.mask[2 * slot] = make_uint4(m[0], m[1], m[2], m[3]);
+      v.mask[2 * slot + 1] = make_uint4(m[4], m[5], m[6], m[7]);
+    };
+    bool first = (uint32_t)blockIdx.x < n_units;
+    uint32_t gbase = 0;
+    for (;;) {
+      if (lane == 0)
+        s_ctrl[0] = first ? (uint32_t)blockIdx.x
+                          : (uint32_t)(gridDim.x + (atomicAdd(a.queue + 1, 1ull) - a.qbase1));
+      first = false;
+      arrive();
+      hw_barrier();                                                   // claim
+      const uint32_t u = s_ctrl[0];
+      if (u >= n_units) break;
+      const int nq = a.n_ticks;
+      if (lane < TILE) {
+        load_tile((int)u);
+        tick_c(0, gbase);
+      }
+      arrive();
+      hw_barrier();                                                   // C(0) done
+      for (int i = 0; i <= nq; ++i) {
+        if (lane < TILE && i + 1 < nq) tick_c(i + 1, gbase + i + 1);
+        arrive();
+        hw_barrier();
+      }
+      if (lane < TILE && live) publish(nq - 1);
+      arrive();
+      hw_barrier();                                                   // unit end
+      gbase += nq;
+    }
+  } else if (wave == 1) {
+    // ======================= D: the scatter, and the teacher table's answers =====================
+    // With policy actions the teacher's walk of item i posts its table-entry requests (s_treq)
+    // and this wave loads them after its scatter of interval i + 1, then decodes them two barriers
+    // later: a load takes longer than an interval under the store stream, and a load waits only
+    // for this wave's own (it issues no store).  Exactly one load instruction per barrier and the
+    // loop unrolled by two (register sets a, b) keep the wait at vmcnt(1): the set decoded at a
+    // barrier is the one loaded two barriers before, the other stays in flight.
+    // (the 32-bit word holding the u16 entry: a u16 load's zero-extension made the compiler wait
+    // for it right after the load's barrier)
+    const uint32_t* tbase = reinterpret_cast<const uint32_t*>(v.ttab ? v.ttab : v.task_tab);
+    int bk = kBClaim, i = 0, nq = 0, nE = 0;
+    uint32_t u = 0;
+    uint32_t va = 0, vb = 0;                                           // table words in flight
+    int ra = -1, rb = -1;                                              // their label rows (-1: none)
+    int na = 0, nb2 = 0;                                               // 0 no request, 1 low half, 2 high
+    auto decode = [&](uint32_t word, int row, int need) __attribute__((always_inline)) {
+      uint32_t* R = s_rows + row * RW;
+      const uint32_t val = need == 2 ? word >> 16 : word & 0xffffu;
+      if (need) {
+        int err = 0, label = -2;
+        if (val & 0x8000u) label = go_leaf_action((val & 0x4000u) != 0, (int)((val >> 10) & 7u) - 1,
+                                                  (int)(val & 0x3ffu) - 1, err);
+        else err = CRAFT_EINVARIANT;                                   // (a reachable grid has its entry)
+        R[4 + lane] = (uint32_t)label;
+        if (err) {                                                     // latched at the end (no VMEM here)
+          uint32_t exp = 0u;
+          if (__hip_atomic_compare_exchange_strong(&s_ctrl[3], &exp, 1u + R[2] * TILE + lane, __ATOMIC_RELAXED,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            s_ctrl[4] = (uint32_t)err;
+        }
+      }
+      const uint32_t cnt = (uint32_t)__popcll(__ballot(need != 0));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0 && cnt)
+        __hip_atomic_fetch_add(&R[0], 0u - cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    // one barrier's work with register set (val, row, need); false after the last claim
+    auto d_slot = [&](uint32_t& val, int& row, int& need) __attribute__((always_inline)) -> bool {
+      if (row >= 0) decode(val, row, need);
+      if (bk == kBTick && i < nq && want_obs) {                        // D(i)
+        const int e = lane % TILE;
+        const uint32_t ag = s_agent[(i & 1) * TILE + e];
+        if (e < nE && ((ag >> 24) & 1u))
+          scatter_env_part<WIN, P>(v, s_grid + (i & 1) * TILE * GS + e * GS,
+                                   s_inv + (i & 1) * TILE * kInvStride + e * kInvStride, ag,
+                                   s_obs + (i & 1) * obs_buf + e * F, lane / TILE);
+      }
+      row = -1;
+      uint32_t req = ~0u;
+      if (!lsync && bk == kBTick && i >= 1) {                          // item i - 1's requests
+        const uint32_t r = s_ctrl[5 + ((i - 1) & 1)];
+        if (r != ~0u) {
+          row = (int)r;
+          if (lane < TILE) req = s_treq[((i - 1) & 1) * TILE + lane];
+        }
+      }
+      need = req == ~0u ? 0 : 1 + (int)(req & 1u);
+      val = tbase[req == ~0u ? 0u : req >> 1];                         // every barrier: one load
+      arrive();
+      hw_barrier();
+      // the next barrier (plain selects: a branchy update here left i and nq in scratch memory)
+      const int b0 = bk;
+      if (b0 == kBClaim) {
+        u = __builtin_amdgcn_readfirstlane(s_ctrl[0]);
+        if (u >= n_units) return false;
+      }
+      nq = a.n_ticks;
+      nE = (int)min((int64_t)TILE, n - (int64_t)u * TILE);
+      i = b0 == kBC0 ? 0 : (b0 == kBTick ? i + 1 : i);
+      bk = b0 == kBClaim ? kBC0 : b0 == kBC0 ? kBTick : b0 == kBTick ? (i > nq ? kBEnd : kBTick) : kBClaim;
+      return true;
+    };
+    for (;;) {
+      if (!d_slot(va, ra, na)) break;
+      if (!d_slot(vb, rb, nb2)) break;
+    }
+    if (ra >= 0) decode(va, ra, na);                                   // the sets still in flight
+    if (rb >= 0) decode(vb, rb, nb2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0 && s_ctrl[3]) latch_error(v.err, (int)s_ctrl[4], (int64_t)s_ctrl[3] - 1);
+  } else if (wave < TW) {
+    // =============================== E: the stores =============================================
+    const int et = tid - 128;
+    uint32_t h = 0;                                                    // wave 2: the next item to store
+    // wave 2: store the label rows that are complete, in item order (at most `reps` now)
+    auto store_rows = [&](int reps) __attribute__((always_inline)) {
+      for (int rep = 0; rep < reps; ++rep) {
+        uint32_t* R = s_rows + (h & (kRtRows - 1)) * RW;
+        const uint32_t c = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&R[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const uint32_t tag = __builtin_amdgcn_readfirstlane(R[1]);
+        if (tag == h + 1 && c == kRowFill) {
+          uint32_t won = 0;
+          if (lane == 0) {
+            uint32_t exp = kRowFill;
+            won = __hip_atomic_compare_exchange_strong(&R[0], &exp, kRowStoring, __ATOMIC_ACQUIRE,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1u : 0u;
+          }
+          if (!__builtin_amdgcn_readfirstlane(won)) break;
+          const int t = (int)R[2];
+          const int64_t r = (int64_t)R[3];
+          const int nE = (int)min((int64_t)TILE, n - (int64_t)t * TILE);
+          const int lab = lane < TILE ? (int)R[4 + lane] : 0;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_store(&R[0], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (a.labels && lane < nE) a.labels[r * n + (int64_t)t * TILE + lane] = lab;
+          ++h;
+        } else if (tag > h + 1) {
+          ++h;                                                         // (not expected: rows are stored here)
+        } else {
+          break;
+        }
+      }
+    };
+    auto e_barrier = [&]() __attribute__((always_inline)) {
+      arrive();
+      if (wave == 2) {
+        // keep storing until the teacher has arrived too (it may wait for a free row)
+        for (uint32_t spins = 0; arrivals() < (uint32_t)NWAVE * (nb + 1); ++spins) {
+          store_rows(1);
+          __builtin_amdgcn_s_sleep(1);
+          if (spins > kRtSpinCap) {                                    // never hang
+            latch_error(v.err, CRAFT_EINVARIANT, rt_where(2, h, s_rows[(h & (kRtRows - 1)) * RW]));
+            break;
+          }
+        }
+      }
+      hw_barrier();
+    };
+    uint32_t gbase = 0;
+    for (;;) {
+      e_barrier();
+      const uint32_t u = s_ctrl[0];
+      if (u >= n_units) break;
+      const int nq = a.n_ticks;
+      gbase += nq;
+      const int64_t env0 = (int64_t)u * TILE;
+      const int nE = (int)min((int64_t)TILE, n - env0);
+      e_barrier();
+      for (int i = 0; i <= nq; ++i) {
+        if (i >= 1 && want_obs) {
+          const int64_t r = (a.tick0 + i - 1) % a.ring;
+          void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * (v.obs_fmt == CRAFT_OBS_F32 ? 4 : v.obs_fmt == CRAFT_OBS_BF16 ? 2 : 1);
+          uint8_t* rows = s_obs + ((i - 1) & 1) * obs_buf;
+          switch (v.obs_fmt) {
+            case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, NE, true>(rows, out, env0, F, nE, v.obs_policy, et); break;
+            case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, NE, true>(rows, out, env0, F, nE, v.obs_policy, et); break;
+            default: stream_obs<CRAFT_OBS_F32, NE, true>(rows, out, env0, F, nE, v.obs_policy, et); break;
+          }
+        }
+        if (wave == 2) store_rows(2);
+        e_barrier();
+      }
+      e_barrier();
+    }
+    // after the last barrier the teacher finishes the BFS jobs left; every label row is stored
+    // here, in item order (the teacher stores nothing)
+    if (wave == 2)
+      for (uint32_t spins = 0; h < gbase; ++spins) {
+        store_rows(kRtRows);
+        __builtin_amdgcn_s_sleep(1);
+        if (spins > kRtSpinCap) {                                      // never hang
+          latch_error(v.err, CRAFT_EINVARIANT, rt_where(3, h, s_rows[(h & (kRtRows - 1)) * RW]));
+          break;
+        }
+      }
+  } else {
+    // =============================== T: the teacher ============================================
+    const int ql = lane & 3;
+    const Bits<NW> valid = brange<NW>(0, C - 2 * H);                  // the band of columns 1 .. W-2
+    QuadBfs<NW> q;
+    uint32_t jhead = 0, jtail = 0;                                     // the job queue (wave-uniform)
+    // ---- one BFS level for every quad (a new job for an idle quad first) ----
+    auto finish = [&](int label, int err) __attribute__((always_inline)) {
+      // lane 0 of the quad: the label into its row, one pending label fewer
+      if (ql == 0) {
+        const int row = (q.meta >> 11) & 7, env = (q.meta >> 14) & 63;
+        uint32_t* R = s_rows + row * RW;
+        R[4 + env] = (uint32_t)label;
+        if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + env);
+        __hip_atomic_fetch_add(&R[0], 0xffffffffu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      q.ph = kQIdle;
+    };
+    auto done_go = [&](bool ok, int fa, int len) __attribute__((always_inline)) {
+      int err = 0;
+      const int label = go_leaf_action(ok, fa, len, err);
+      finish(label, err);
+    };
+    const int dla = ql == 0 ? -1 : ql == 1 ? 1 : ql == 2 ? -H : H;    // this lane's action: cell shift
+    auto qp0 = [&]() __attribute__((always_inline)) -> int { return (int)(q.meta & 0xffu); };
+    auto qd0 = [&]() __attribute__((always_inline)) -> int { return (int)((q.meta >> 8) & 3u); };
+    auto blocked = [&]() __attribute__((always_inline)) -> Bits<NW> {   // blk[p] = occ[p + dla]
+      Bits<NW> b = bshift_var(bandn(valid, q.fr), -dla);
+      if (ql == 2) b = bor(b, band_edge_lo<NW>(valid, H));           // the border columns left out
+      if (ql == 3) b = bor(b, band_edge_hi<NW>(valid, H));           // of the band
+      return b;
+    };
+    auto raises = [&]() __attribute__((always_inline)) -> bool {   // base.py:31: unreachable after reachable
+      const Bits<NW> unreached = bandn(q.tgt, q.claimed);
+      return bany(unreached) && blowest(q.claimed) < bhighest(unreached);
+    };
+    auto bwd_final = [&]() __attribute__((always_inline)) {
+      const int p0 = qp0();
+      const int q0 = p0 + dla;
+      const int qq = btest(q.fr, q0) ? q0 : p0;
+      const bool ok = !(qq == p0 && ql == qd0()) && btest(q.V, qq);
+      const uint32_t quad = (uint32_t)(__ballot(ok) >> (lane & ~3)) & 0xfu;
+      done_go(true, quad ? __ffs(quad) - 1 : -1, q.L);
+    };
+    auto bwd_init = [&]() __attribute__((always_inline)) {
+      if (q.L == 0) { done_go(true, -1, 0); return; }
+      const int qc = q.chosen - dla;
+      q.U = (qc >= 0) ? band(bbit<NW>(qc), q.fr) : bzero<NW>();
+      q.V = q.U;
+      q.k = 1;
+      if (q.k < q.L) q.ph = kQBwd;
+      else bwd_final();
+    };
+    auto after_fwd = [&]() __attribute__((always_inline)) {
+      if (q.L < 0) { done_go(true, -1, -1); return; }                 // no target reachable: None
+      if (bany(bandn(q.tgt, q.claimed))) {
+        if (((q.meta >> 10) & 1u) && btest(q.fr, qp0())) {
+          // connected free cells: a target is reachable iff it has a free neighbour
+          q.claimed = bor(q.claimed, band(quad_or(bshift_var(q.fr, dla)), q.tgt));
+          if (raises()) { done_go(false, -1, -1); return; }
+          bwd_init();
+        } else {
+          q.U = bor(quad_or(q.V), bbit<NW>(qp0()));                    // flood from the visited cells
+          q.ph = kQReach;
+        }
+      } else {
+        bwd_init();
+      }
+    };
+    auto take_jobs = [&]() __attribute__((always_inline)) {
+      const uint32_t avail = jtail - jhead;
+      if (avail == 0) return;
+      const uint64_t idle = __ballot(q.ph == kQIdle && ql == 0);
+      if (!idle) return;
+      const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
+      const uint32_t taken = min(avail, (uint32_t)__popcll(idle));
+      if (q.ph == kQIdle && rank < avail) {
+        const uint32_t* J = s_jobs + ((jhead + rank) % kRtQueue) * JW;
+        Bits<NW> occ;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) { occ.w[i] = J[i]; q.tgt.w[i] = J[NW + i]; }
+        q.meta = J[2 * NW];
+        q.fr = bandn(valid, occ);
+        const int d0 = qd0(), p0 = qp0();
+        const int dl0 = d0 == 0 ? -1 : d0 == 1 ? 1 : d0 == 2 ? -H : H;
+        q.claimed = bzero<NW>();
+        q.L = -1;
+        q.chosen = -1;
+        const int f0 = p0 + dl0;                                       // the start already faces a target
+        if (f0 >= 0 && btest(q.tgt, f0)) {
+          q.L = 0;
+          q.chosen = f0;
+          q.claimed = bbit<NW>(f0);
+        }
+        q.V = (ql == d0) ? bbit<NW>(p0) : bzero<NW>();
+        q.U = bbit<NW>(p0);
+        q.k = 1;
+        if (bany(bandn(q.tgt, q.claimed)) && q.L < 0) q.ph = kQFwd;
+        else after_fwd();
+      }
+      jhead += taken;
+    };
+    auto step = [&]() __attribute__((always_inline)) {
+#ifdef RT_NO_STEP
+      return;
+#endif
+      take_jobs();
+      if (q.ph == kQFwd) {
+        const Bits<NW> nxt = bandn(bor(band(bshift_var(q.U, dla), q.fr), band(q.U, blocked())), q.V);
+        q.V = bor(q.V, nxt);
+        const Bits<NW> nU = quad_or(nxt);
+        if (!bany(nU)) {
+          after_fwd();                                                 // every reachable state visited
+        } else {
+          uint32_t face = 0;
+          const Bits<NW> fa = bshift_var(q.tgt, -dla);                 // fa[p] = tgt[p + dla]
+#pragma unroll
+          for (int i = 0; i < NW; ++i) face |= nxt.w[i] & fa.w[i];
+          bool hitany = false;
+          if ((uint32_t)(__ballot(face != 0) >> (lane & ~3)) & 0xfu) {
+            const Bits<NW> hit = bandn(quad_or(band(bshift_var(nxt, dla), q.tgt)), q.claimed);
+            if (bany(hit)) {
+              q.claimed = bor(q.claimed, hit);
+              q.L = q.k;
+              q.chosen = blowest(hit);
+              hitany = true;
+            }
+          }
+          if (hitany) {
+            after_fwd();
+          } else {
+            q.U = nU;
+            ++q.k;
+          }
+        }
+      }
+      if (q.ph == kQReach) {
+        const Bits<NW> adj = quad_or(bshift_var(q.U, dla));          // cells next to the reached set
+        q.claimed = bor(q.claimed, band(adj, q.tgt));
+        if (!bany(bandn(q.tgt, q.claimed))) {
+          bwd_init();
+        } else {
+          const Bits<NW> grow = bandn(band(adj, q.fr), q.U);
+          if (!bany(grow)) {
+            if (raises()) done_go(false, -1, -1);
+            else bwd_init();
+          } else {
+            q.U = bor(q.U, grow);
+          }
+        }
+      }
+      if (q.ph == kQBwd) {
+        // predecessors, any direction: moved here or turned in place (blocked)
+        const Bits<NW> P2 = quad_or(bor(band(bshift_var(q.U, -dla), q.fr), band(q.U, blocked())));
+        q.U = bandn(P2, q.V);
+        q.V = bor(q.V, q.U);
+        ++q.k;
+        if (q.k >= q.L) bwd_final();
+      }
+    };
+    auto busy = [&]() __attribute__((always_inline)) -> bool {
+      return jtail != jhead || __ballot(q.ph != kQIdle) != 0;
+    };
+    auto row_ctrl = [&](int row) __attribute__((always_inline)) -> uint32_t {
+      return __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&s_rows[row * RW], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    // queue n jobs: lanes with `mine` write theirs (band bitsets of `row32` for `kind`) in lane order
+    auto push_jobs = [&](uint64_t mask, bool mine, const uint8_t* row8, int kind, int p0, int d0, int cn,
+                         int row) __attribute__((always_inline)) {
+      if (mine) {
+        const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        uint32_t* J = s_jobs + ((jtail + rank) % kRtQueue) * JW;
+        const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        Bits<NW> occ, tgt;
+        band_bits<NW, 1>(reinterpret_cast<const uint32_t*>(row8), (C + 3) >> 2, C, H, m0, (uint32_t)kind, 0, occ, tgt);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) { J[i] = occ.w[i]; J[NW + i] = tgt.w[i]; }
+        J[2 * NW] = rt_job_meta(p0, d0, cn, row, lane);
+      }
+      jtail += (uint32_t)__popcll(mask);
+    };
+
+    // The teacher's schedule is a sequence of duties, each run once its condition holds; whenever
+    // the next duty has to wait, the wave runs one BFS level (the single step() site: the BFS
+    // state stays in registers instead of being spilled around several inlined copies).
+    enum { D_BAR, D_DECODE, D_DECODE_JOBS, D_WALK, D_WALK_JOBS, D_SYNC, D_DRAIN, D_EXIT };
+    enum { B_CLAIM, B_C0, B_TICK, B_END };
+    int duty = D_BAR, bkind = B_CLAIM;
+    int i = 0, nq = 0, nE = 0;
+    uint32_t u = 0, gbase = 0;
+    // the walk's per-lane results between its two duties, and the table answer carried to the
+    // decode (the next interval with policy actions, the same one with label actions)
+    int w_label = 0, w_need = 0;
+    uint32_t w_key = 0;                                                // as tt_key
+    uint32_t tt_val = 0, tt_key = 0;                                   // tt_key: p0 | dir<<8 | kind<<12 | conn<<20
+    bool tt_need = false;
+    int tt_row = 0, d_fall = 0;
+    auto next_in_tick = [&]() __attribute__((always_inline)) -> int {   // after the barrier opening interval i
+      return i < nq ? D_WALK : D_BAR;
+    };
+    uint32_t steps_run = 0;                                            // BFS levels this launch
+    for (uint32_t idle_spins = 0;;) {
+      bool wait = false;
+      switch (duty) {
+        case D_BAR: {
+          if (arrivals() < (uint32_t)NWAVE * nb + (NWAVE - 1)) { wait = true; break; }
+          arrive();
+          hw_barrier();
+          if (bkind == B_CLAIM) {
+            u = s_ctrl[0];
+            if (u >= n_units) { duty = D_DRAIN; break; }
+            nq = a.n_ticks;
+            nE = (int)min((int64_t)TILE, n - (int64_t)u * TILE);
+            bkind = B_C0;
+          } else if (bkind == B_C0) {
+            i = 0;
+            bkind = B_TICK;
+            duty = next_in_tick();
+          } else if (bkind == B_TICK) {
+            if (++i > nq) bkind = B_END;
+            else duty = next_in_tick();
+          } else {
+            gbase += nq;
+            bkind = B_CLAIM;
+          }
+          break;
+        }
+        case D_DECODE: {                                               // the table answers of the last walk
+          d_fall = 0;
+          const uint64_t bn = __ballot(tt_need);
+          if (tt_need) {
+            uint32_t* R = s_rows + tt_row * RW;
+            if (tt_val & 0x8000u) {
+              int err = 0;
+              R[4 + lane] = (uint32_t)go_leaf_action((tt_val & 0x4000u) != 0, (int)((tt_val >> 10) & 7u) - 1,
+                                                      (int)(tt_val & 0x3ffu) - 1, err);
+              if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + lane);
+            } else {
+              d_fall = 1;                                              // not computed: search the pristine row
+            }
+          }
+          const uint64_t bf = __ballot(d_fall != 0);
+          const uint32_t resolved = (uint32_t)__popcll(bn) - (uint32_t)__popcll(bf);
+          if (lane == 0 && resolved)
+            __hip_atomic_fetch_add(&s_rows[tt_row * RW], 0u - resolved, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          tt_need = false;
+          duty = bf ? D_DECODE_JOBS : D_SYNC;
+          break;
+        }
+        case D_DECODE_JOBS: {
+          const uint64_t bf = __ballot(d_fall != 0);
+          if (jtail - jhead + (uint32_t)__popcll(bf) > (uint32_t)kRtQueue) { wait = true; break; }
+          push_jobs(bf, d_fall != 0, s_pristine + lane * GS, (tt_key >> 12) & 0xff, tt_key & 0xff,
+                    (tt_key >> 8) & 3, (tt_key >> 20) & 1, tt_row);
+          d_fall = 0;
+          duty = D_SYNC;
+          break;
+        }
+        case D_WALK: {                                                 // item g = gbase + i, buffer i & 1
+          const uint32_t g = gbase + (uint32_t)i;
+          const int row = (int)(g & (kRtRows - 1));
+          if (row_ctrl(row) != 0u) { wait = true; break; }             // wave 2 frees it at the latest at the barrier
+          uint32_t* R = s_rows + row * RW;
+          const int p = i & 1;
+          w_label = -2;
+          w_need = 0;                                                  // 1: a table answer, 2: a BFS job
+          uint32_t req = ~0u;                                          // (policy actions) the ttab index asked
+          if (lane < nE) {
+            const uint32_t ag = s_agent[p * TILE + lane];
+            const uint32_t ti = s_tinfo[p * TILE + lane];
+            if (((ag >> 24) & 1u) && ((ag >> 25) & 1u)) {
+              w_label = -1;                                            // frozen: the label of a done env
+            } else if ((ag >> 24) & 1u) {
+              const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+              const uint8_t* gr = s_grid + p * TILE * GS + lane * GS;
+              const int facing = gr[(x + dir_dx(dir)) * H + (y + dir_dy(dir))];
+              int err = 0, kind = 0;
+#if defined(RT_ABL) && (RT_ABL & 1)                                   // ablation builds only: no walk
+              w_label = CRAFT_STOP + (facing & 0);
+#else
+              w_label = hint_leaf(s_task, s_tsub, s_inv + p * TILE * kInvStride + lane * kInvStride, facing,
+                                  (int)(ti & 0xff), err, kind);
+#endif
+              if (err) latch_error(v.err, err, (int64_t)u * TILE + lane);
+              w_key = (uint32_t)(x * H + y - H) | ((uint32_t)dir << 8) | ((uint32_t)(kind & 0xff) << 12) |
+                      (((ti >> 8) & 1u) << 20);
+              if (w_label == kTeachGo) {
+                // the table's row for this grid: the pool row minus the listed cells it cleared
+                const int ncl = (int)(ag >> 26);
+                const int trow = v.ttab && a.use_table && ncl < 63
+                                     ? tt_index(v, (int)(ti >> 10), s_tcell[2 * lane], s_tcell[2 * lane + 1], ncl,
+                                                [&](int c) { return gr[c] == 0; })
+                                     : -1;
+                const int sl = trow >= 0 ? tt_slot_of(v, kind) : -1;
+                w_need = sl >= 0 ? 1 : 2;
+#if defined(RT_ABL) && (RT_ABL & 2)                                   // ablation: no table loads
+                if (w_need == 1) { w_need = 0; w_label = CRAFT_STOP; }
+#endif
+#if defined(RT_ABL) && (RT_ABL & 4)                                   // ablation: no BFS jobs
+                if (w_need == 2) { w_need = 0; w_label = CRAFT_STOP; }
+#endif
+                if (w_need == 1) {
+                  const uint32_t idx = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
+                  if (lsync) {
+                    tt_val = v.ttab[idx];                              // decoded in this interval
+                    tt_key = w_key;
+                  } else {
+                    req = idx;                                         // the scatter wave loads it
+                  }
+                }
+              }
+            }
+          }
+          if (lane < TILE) R[4 + lane] = w_need ? 0u : (uint32_t)w_label;
+          if (lane == 0) {
+            R[1] = g + 1;
+            R[2] = u;
+            R[3] = (uint32_t)((a.tick0 + i) % a.ring);
+          }
+          if (!lsync) {
+            const bool any_req = __ballot(req != ~0u) != 0;          // (the whole wave votes)
+            if (lane < TILE) s_treq[p * TILE + lane] = req;
+            if (lane == 0) s_ctrl[5 + p] = any_req ? (uint32_t)row : ~0u;
+          }
+          tt_need = lsync && w_need == 1;
+          tt_row = row;
+          duty = D_WALK_JOBS;
+          break;
+        }
+        case D_WALK_JOBS: {
+          const uint64_t bj = __ballot(w_need == 2);
+          if (jtail - jhead + (uint32_t)__popcll(bj) > (uint32_t)kRtQueue) { wait = true; break; }
+          const int row = (int)((gbase + (uint32_t)i) & (kRtRows - 1));
+          push_jobs(bj, w_need == 2, s_grid + (i & 1) * TILE * GS + lane * GS, (w_key >> 12) & 0xff, w_key & 0xff,
+                    (w_key >> 8) & 3, (w_key >> 20) & 1, row);
+          // the row's control word last: the labels still pending (0 = complete)
+          const uint32_t pending = (uint32_t)__popcll(__ballot(w_need != 0));
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0)
+            __hip_atomic_store(&s_rows[row * RW], kRowFill | pending, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          duty = lsync ? D_DECODE : D_BAR;
+          break;
+        }
+        case D_SYNC: {                                                 // label actions: item i complete
+          const int row = (int)((gbase + (uint32_t)i) & (kRtRows - 1));
+          if ((row_ctrl(row) & ~kRowFill) != 0u) { wait = true; break; }
+          if (lane == 0)
+            __hip_atomic_store(&s_ctrl[2], gbase + (uint32_t)i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          duty = D_BAR;
+          break;
+        }
+        case D_DRAIN:                                                  // after the last barrier: the jobs left
+          if (busy()) wait = true;
+          else duty = D_EXIT;
+          break;
+        default:
+          break;
+      }
+      if (duty == D_EXIT) break;
+      if (wait) {
+        if (busy()) {
+          step();
+          idle_spins = 0;
+          if (++steps_run > (1u << 22)) {                              // never hang the GPU (~2 s)
+            latch_error(v.err, CRAFT_EINVARIANT, rt_where(5, gbase + (uint32_t)i, (uint32_t)duty));
+            break;
+          }
+        } else {
+          __builtin_amdgcn_s_sleep(1);
+          if (++idle_spins > kRtSpinCap) {                             // never hang the GPU
+            latch_error(v.err, CRAFT_EINVARIANT,
+                        rt_where(4, gbase + (uint32_t)i, ((uint32_t)duty << 24) | s_rows[((gbase + i) & (kRtRows - 1)) * RW]));
+            break;
+          }
+        }
+      }
+    }
+  }
+
+  if (tid == 0) {
+    unsigned long long* srow = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
+    atomicAdd(srow + 0, (unsigned long long)n_succ);
+    atomicAdd(srow + 1, (unsigned long long)n_end);
+    atomicAdd(srow + 2, (unsigned long long)n_step);
+  }
+}
+
+}  // namespace craft

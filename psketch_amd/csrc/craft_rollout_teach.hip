@@ -1,0 +1,65 @@
+// craft_rollout_teach.hip — launches of the teacher-labelled K-tick rollout kernel
+// (craft_rollout_teach.h), one instantiation per window and BFS word count.
+#include <algorithm>
+
+#include "craft_rollout_teach.h"
+
+namespace craft {
+
+template <int WIN, int NW>
+static hipError_t launch_rt_one(const SimView& v, const RolloutArgs& a, hipStream_t st) {
+  constexpr int TILE = rt_tile(WIN);
+  const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
+  if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
+  const size_t lds = (size_t)rt_lds(TILE, v.GS, v.F, NW).bytes;
+  auto kern = rollout_teach_kernel<WIN, TILE, NW>;
+  {
+    const hipError_t e = ensure_lds<&rollout_teach_kernel<WIN, TILE, NW>>(lds);
+    if (e != hipSuccess) return e;
+  }
+  // persistent workgroups: what the chip holds at once, spread so that every workgroup runs the
+  // same number of tiles
+  static int resident = 0;
+  static size_t resident_lds = 0;
+  if (resident == 0 || resident_lds != lds) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kRtThreads, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+      cus = 256;
+    resident = per_cu * cus;
+    resident_lds = lds;
+  }
+  const int64_t rounds = (tiles + resident - 1) / resident;
+  const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;   // stats_part rows
+  const int64_t grid = std::min<int64_t>((tiles + rounds - 1) / rounds, rows);
+  if (a.grid_out) *a.grid_out = grid;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kRtThreads), lds, st, v, a);
+  return hipGetLastError();
+}
+
+template <int WIN>
+static hipError_t launch_rt_win(int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
+  // nw = 32-bit words per BFS cell set (the band of columns 1 .. W-2): 8x8 -> 2, 10x10 -> 3 (run
+  // as 4), 12x12 -> 4, up to 15x15 -> 7 (run as 8)
+  if (nw <= 2) return launch_rt_one<WIN, 2>(v, a, st);
+  if (nw <= 4) return launch_rt_one<WIN, 4>(v, a, st);
+  return launch_rt_one<WIN, 8>(v, a, st);
+}
+
+hipError_t launch_rollout_teach(int win, int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
+#ifdef CRAFT_RT_ONE       // diagnostic builds: the 3x3, 12x12 instantiation only (compile time)
+  (void)win;
+  (void)nw;
+  return launch_rt_one<3, 4>(v, a, st);
+#else
+  switch (win) {
+    case 3: return launch_rt_win<3>(nw, v, a, st);
+    case 5: return launch_rt_win<5>(nw, v, a, st);
+    default: return launch_rt_win<7>(nw, v, a, st);
+  }
+#endif
+}
+
+}  // namespace craft

@@ -15,8 +15,9 @@
 namespace craft {
 hipError_t launch_tile(int mode, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
                        hipStream_t st);
-hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
+hipError_t launch_teacher(int nw, int lanes, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st);
+hipError_t launch_rollout_teach(int win, int nw, const SimView& v, const RolloutArgs& a, hipStream_t st);
 hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, const int8_t* success,
                             const int32_t* seqs, int32_t ticks, int64_t n, int32_t* dist_out,
                             uint8_t* is_get_out, int32_t* n_actions_out, int32_t* flags, hipStream_t st);
@@ -149,9 +150,14 @@ struct craft_sim {
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   uint16_t* d_ttab = nullptr;       // the teacher table (craft_teach.h), or null
-  // whether craft_step_teach's kernels read the table (CRAFT_TT_FUSED: 0 never, 1 always, 2 auto:
-  // when the launch rewrites the previous launch's observation buffer, as a trainer's loop does)
-  int tt_mode = 2;
+  uint32_t* d_ttcells = nullptr;    // [pool_capacity][2]: each row's listed clearable cells
+  int tt_nslot = 0;                 // target-kind slots of the table
+  bool tt_decided = false;          // its size is fixed at the first pool load (ensure_table)
+  // craft_sim_tune_teach: which teacher reads the table (0 auto: craft_step_teach when the launch
+  // rewrites the previous launch's observation buffer, as a trainer's loop does, every other
+  // teacher always; 1 always; 2 never), and teacher lanes per query (0 = each kernel's default)
+  int teach_table = 0;
+  int teach_lanes = 0;
   const void* last_teach_obs = nullptr;
   int32_t tt_kinds[16] = {};        // its slots' target kinds
   SimView view{};
@@ -261,14 +267,22 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
   // 128-env workgroups fill the chip, else the one-tile kernel
   if (k == 0) k = (w3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0 && s->n_envs >= 32768) ? 2 : 1;
   if (k == 2 && !(w3 && s->tile == craft::kMaxTileEnvs && s->resident_cap == 0)) k = 1;
-  static const int tl2 = (getenv("CRAFT_TEACH_LANES") && atoi(getenv("CRAFT_TEACH_LANES")) == 4) ? 4 : 2;
-  static const int tl1 = [] {
-    const char* e = getenv("CRAFT_TEACH_LANES");
-    const int x = e ? atoi(e) : 4;
-    return (x == 1 || x == 2) ? x : 4;
-  }();
+  // teacher lanes per env (craft_sim_tune_teach): the two-tile kernel runs pairs (or quads), the
+  // one-tile kernel quads (or pairs, or one lane)
+  const int tl2 = s->teach_lanes == 4 ? 4 : 2;
+  const int tl1 = (s->teach_lanes == 1 || s->teach_lanes == 2) ? s->teach_lanes : 4;
   if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
   else { *kernel = 1; *envs = craft::kMaxTileEnvs; *lanes = tl1; }
+}
+
+// The view a teacher launch gets: the table hidden when craft_sim_tune_teach says never.
+SimView teach_view(const craft_sim* s) {
+  SimView v = s->view;
+  if (s->teach_table == 2) {
+    v.ttab = nullptr;
+    v.tt_slots = 0;
+  }
+  return v;
 }
 
 int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* what) {
@@ -276,6 +290,44 @@ int launch(craft_sim* s, int mode, const TileArgs& a, void* stream, const char* 
                                     reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, what);
   return CRAFT_OK;
+}
+
+// The cells of a grid that grab, bridge or axe can clear (craft.py:383-410): non-empty cells of a
+// grabbable, water or stone kind.
+int clearable_cells(const craft_config_t& cfg, const uint8_t* g, int C) {
+  int m = 0;
+  for (int c = 0; c < C; ++c) {
+    const int k = g[c], cls = k < CRAFT_MAX_KINDS ? cfg.kind_class[k] : CRAFT_KIND_INERT;
+    m += k != 0 && (cls == CRAFT_KIND_GRABBABLE || cls == CRAFT_KIND_WATER || cls == CRAFT_KIND_STONE);
+  }
+  return m;
+}
+
+// The teacher table's size, fixed at the first pool load from the most clearable cells any row of
+// that load has (every grid an env of a row can reach is the row minus a subset of them): tt_m =
+// that many (at most 8), fewer while pool_capacity rows x 2^tt_m subsets x slots x 4 directions x C
+// cells of u16 exceed 1 GiB or 2^21 table rows (the kernels pack a table row into 21 bits).  12x12
+// craft_medium: 6 clearable cells per row, 6 slots: 442 KB per row, 453 MB for 1024 rows.  A row
+// with more clearable cells lists its first tt_m; an env that clears another one has no table row
+// and its queries run the BFS.  Without room for even the pristine grids (tt_m 0) the table is off.
+void ensure_table(craft_sim* s, int max_clearable) {
+  if (s->tt_decided) return;
+  s->tt_decided = true;
+  const int C = s->view.C;
+  if (s->tt_nslot == 0) return;
+  const size_t budget = (size_t)1 << 30;
+  int m = std::min(8, std::max(0, max_clearable));
+  auto bytes = [&](int mm) { return ((size_t)s->pool_capacity << mm) * s->tt_nslot * 4 * C * sizeof(uint16_t); };
+  while (m >= 0 && (bytes(m) > budget || ((int64_t)s->pool_capacity << m) >= ((int64_t)1 << 21))) --m;
+  if (m < 0) return;
+  if (hipMalloc(&s->d_ttab, bytes(m)) != hipSuccess) {
+    (void)hipGetLastError();
+    s->d_ttab = nullptr;                  // no table: every query runs the BFS (same results)
+    return;
+  }
+  s->view.ttab = s->d_ttab;
+  s->view.tt_slots = s->tt_nslot;
+  s->view.tt_nsub = 1 << m;
 }
 
 }  // namespace
@@ -317,9 +369,6 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   // wave count is rounded up to the workgroup's 4)
   s->n_tiles = (n_envs + craft::kMinTileEnvs - 1) / craft::kMinTileEnvs + 4;
   s->tile = default_tile(cfg->window_width);
-  const char* ttf_env = getenv("CRAFT_TT_FUSED");
-  s->tt_mode = ttf_env ? std::min(std::max(atoi(ttf_env), 0), 2) : 2;
-  s->view.tt_fused = s->tt_mode == 1;
   const int W = cfg->width, H = cfg->height, K = cfg->n_kinds, F = cfg->n_features;
   const int C = W * H, CS = (C + 15) & ~15;
   const int GS = CS + 4;                  // odd dword stride: lane-private rows hit distinct banks
@@ -368,9 +417,9 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_sync, s->sync_bytes);
   ALLOC(s->d_sync_graph, s->sync_bytes);      // craft_rollout launches captured into a graph
   // The teacher table: one slot per kind some go[] or get[] task targets (teach_env's BFS kinds
-  // and the rollout summary's), 4 directions x C start cells per pool row, u16 entries.  Off
-  // (null: every query searches) past 1 GiB, past 2^21 rows (s_tinfo packs the row in 21 bits)
-  // or with CRAFT_TEACH_TABLE=0 (the A/B and parity switch).
+  // and the rollout summary's); its size is fixed at the first pool load (ensure_table).
+  // craft_sim_tune_teach(.., table 2) stops every teacher reading it (the parity switch).
+  ALLOC(s->d_ttcells, (size_t)pool_capacity * 2 * sizeof(uint32_t));
   {
     int nslot = 0;
     uint64_t smap[2] = {~0ull, ~0ull};
@@ -384,14 +433,9 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
       smap[k >> 4] |= (uint64_t)nslot << (4 * (k & 15));
       s->tt_kinds[nslot++] = k;
     }
-    const char* tt_env = getenv("CRAFT_TEACH_TABLE");
-    const size_t tt_bytes = (size_t)pool_capacity * nslot * 4 * C * sizeof(uint16_t);
-    if (nslot > 0 && pool_capacity < (1 << 21) && tt_bytes <= ((size_t)1 << 30) && !(tt_env && atoi(tt_env) == 0)) {
-      ALLOC(s->d_ttab, tt_bytes);
-      s->view.tt_slots = nslot;
-      s->view.tt_slot[0] = smap[0];
-      s->view.tt_slot[1] = smap[1];
-    }
+    s->tt_nslot = nslot;
+    s->view.tt_slot[0] = smap[0];
+    s->view.tt_slot[1] = smap[1];
   }
 #undef ALLOC
   if ((e = hipMemcpy(s->d_task, task_tab.data(), sizeof(uint16_t) * task_tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
@@ -412,7 +456,9 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.task_sub = s->d_task_sub;
   v.stats_part = s->d_stats;
   v.err = s->d_err;
-  v.ttab = s->d_ttab;
+  v.ttab = nullptr;                       // (until the first pool load: ensure_table)
+  v.tt_cells = s->d_ttcells;
+  v.tt_nsub = 1;
   v.n_envs = n_envs;
   v.env_base = env_id_base;
   v.pool_count = 0;
@@ -455,11 +501,17 @@ int craft_sim_tune(craft_sim_t* s, int32_t tile_envs, int32_t max_resident_per_c
   return CRAFT_OK;
 }
 
-int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel) {
+int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel, int32_t lanes, int32_t table) {
   if (!s) return CRAFT_EINVAL;
   if (kernel < 0 || kernel > 2)
     return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: kernel must be 0 (auto), 1 (one-tile) or 2 (two-tile)");
+  if (lanes != 0 && lanes != 1 && lanes != 2 && lanes != 4)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: lanes must be 0 (default), 1, 2 or 4");
+  if (table < 0 || table > 2)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_teach: table must be 0 (auto), 1 (always) or 2 (never)");
   s->teach_kernel = kernel;
+  s->teach_lanes = lanes;
+  s->teach_table = table;
   return CRAFT_OK;
 }
 
@@ -509,6 +561,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_sync);
   (void)hipFree(s->d_sync_graph);
   (void)hipFree(s->d_ttab);
+  (void)hipFree(s->d_ttcells);
   delete s;
   return CRAFT_OK;
 }
@@ -579,6 +632,9 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
   }
   HIP_TRY(s, hipSetDevice(s->device));
   if (count) {
+    int maxm = 0;
+    for (int p = 0; p < count; ++p) maxm = std::max(maxm, clearable_cells(s->cfg, grids + (size_t)p * C, C));
+    ensure_table(s, maxm);
     HIP_TRY(s, hipMemcpy(s->d_pool + (size_t)first * CS, staged.data(), staged.size(), hipMemcpyHostToDevice));
     HIP_TRY(s, hipMemcpy(s->d_pool_conn + first, conn.data(), count, hipMemcpyHostToDevice));
     // the rows' teacher-table entries (synchronous, like the load itself)
@@ -621,6 +677,18 @@ int craft_pool_generate(craft_sim_t* s, uint64_t seed, int64_t scenario_id0, int
   for (int i = 0; i < n_workshops; ++i) a.ws[i] = workshop_kind[i];
   a.init_out = init_pos_out;
   HIP_TRY(s, hipSetDevice(s->device));
+  {
+    // the generated rows' clearable cells: n_per_primitive of each clearable primitive kind, and
+    // the clearable workshop kinds
+    auto clearable = [&](int k) {
+      const int cls = s->cfg.kind_class[k];
+      return cls == CRAFT_KIND_GRABBABLE || cls == CRAFT_KIND_WATER || cls == CRAFT_KIND_STONE;
+    };
+    int maxm = 0;
+    for (int i = 0; i < n_primitive_kinds; ++i) maxm += clearable(primitives[i]) ? n_per_primitive : 0;
+    for (int i = 0; i < n_workshops; ++i) maxm += clearable(workshop_kind[i]) ? 1 : 0;
+    if (count) ensure_table(s, maxm);
+  }
   hipError_t e = craft::launch_scenarios(s->view, a, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_pool_generate launch");
   e = craft::launch_teach_table(craft::teach_words(s->view.W, s->view.H), s->view, first, count, s->tt_kinds,
@@ -701,8 +769,8 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   // loop: ring 1, -2.5 us per tick) and go to HBM beside the store stream when every launch
   // writes a fresh buffer (a 16-slot ring: +0.5 us), so auto mode reads them only in the first
   // case (profiles/r04/ab5).
-  SimView v = s->view;
-  if (s->tt_mode == 2) v.tt_fused = (a.obs == nullptr || a.obs == s->last_teach_obs) ? 1 : 0;
+  SimView v = teach_view(s);
+  v.tt_fused = s->teach_table == 1 || (s->teach_table == 0 && (a.obs == nullptr || a.obs == s->last_teach_obs));
   s->last_teach_obs = a.obs;
   if (kernel == 2) {
     e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, nw, s->view.GS, s->view.F), st);
@@ -796,6 +864,72 @@ int craft_rollout(craft_sim_t* s, const int32_t* actions, uint64_t action_seed, 
   return CRAFT_OK;
 }
 
+int craft_rollout_teach(craft_sim_t* s, const craft_rollout_teach_args_t* x, void* stream) {
+  if (!s || !x) return CRAFT_EINVAL;
+  if (x->n_ticks < 0 || x->ring < 1 || x->tick0 < 0)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: need n_ticks >= 0, ring >= 1, tick0 >= 0");
+  if (4 * s->view.C > 1000)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
+  const bool lsync = x->label_actions != 0 || x->behavior_clone != nullptr;
+  if (lsync && !x->label_in)
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: label_actions / behavior_clone need label_in");
+  const int esz = s->view.obs_fmt == CRAFT_OBS_F32 ? 4 : (s->view.obs_fmt == CRAFT_OBS_BF16 ? 2 : 1);
+  if (x->obs && (!aligned16(x->obs) || (x->ring > 1 && (s->n_envs * (int64_t)s->view.F * esz) % 16 != 0)))
+    return fail(s, CRAFT_EINVAL, "craft_rollout_teach: every obs ring slot must be 16-byte aligned");
+  if (x->n_ticks == 0) return CRAFT_OK;
+  craft::RolloutArgs a{};
+  a.actions = x->actions;
+  a.seed = x->action_seed;
+  a.tick0 = x->tick0;
+  a.n_ticks = x->n_ticks;
+  a.ring = x->ring;
+  a.flags = x->flags;
+  a.obs = x->obs;
+  a.reward = x->reward;
+  a.done = x->done;
+  a.sat = x->success;
+  a.chunk = x->n_ticks;                           // one unit per tile: all n_ticks ticks
+  a.label_in = x->label_in;
+  a.bc = x->behavior_clone;
+  a.label_actions = x->label_actions != 0;
+  a.lsync = lsync;
+  a.use_table = s->teach_table != 2;              // auto = always: the reads overlap the stream
+  a.labels = x->labels;
+  a.rec = x->action_record;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // the work-unit counter as craft_rollout's split kernel uses it (queue[1], one claim past the
+  // last unit per workgroup); a captured launch gets the graph's own zeroed counter
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_TRY(s, hipStreamIsCapturing(st, &cap));
+  const bool captured = cap != hipStreamCaptureStatusNone;
+  uint8_t* sync = captured ? s->d_sync_graph : s->d_sync;
+  a.queue = reinterpret_cast<unsigned long long*>(sync);
+  a.tile_done = reinterpret_cast<uint32_t*>(sync + 16);
+  if (captured) {
+    HIP_TRY(s, hipMemsetAsync(sync, 0, s->sync_bytes, st));
+    a.qbase = 0;
+    a.qbase1 = 0;
+  } else {
+    if (!s->sync_zeroed) {
+      HIP_TRY(s, hipMemsetAsync(s->d_sync, 0, s->sync_bytes, st));
+      s->sync_zeroed = true;
+      s->queue_next = 0;
+      s->queue1_next = 0;
+    }
+    a.qbase = s->queue_next;
+    a.qbase1 = s->queue1_next;
+  }
+  int64_t grid = 0;
+  a.grid_out = &grid;
+  SimView v = teach_view(s);
+  v.obs_policy = s->rollout_obs_policy;
+  const int64_t units = (s->n_envs + craft::rt_tile_of(s->cfg.window_width) - 1) / craft::rt_tile_of(s->cfg.window_width);
+  hipError_t e = craft::launch_rollout_teach(s->cfg.window_width, craft::teach_words(s->view.W, s->view.H), v, a, st);
+  if (e != hipSuccess) return hip_fail(s, e, "craft_rollout_teach launch");
+  if (!captured && grid > 0) s->queue1_next += (uint64_t)std::max<int64_t>(units, grid);
+  return CRAFT_OK;
+}
+
 int craft_stats(craft_sim_t* s, int64_t* stats_out, int32_t reset, void* stream) {
   if (!s || !stats_out) return CRAFT_EINVAL;
   hipLaunchKernelGGL(craft::stats_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
@@ -848,7 +982,7 @@ int craft_rollout_distances(craft_sim_t* s, const int32_t* tasks, const int8_t* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(s, hipMemsetAsync(flags_out, 0, 2 * sizeof(int32_t), st));
   if (s->n_envs == 0) return CRAFT_OK;
-  hipError_t e = craft::launch_distances(craft::teach_words(s->view.W, s->view.H), s->view, tasks, success, action_seqs, ticks,
+  hipError_t e = craft::launch_distances(craft::teach_words(s->view.W, s->view.H), teach_view(s), tasks, success, action_seqs, ticks,
                                          s->n_envs, distances_out, is_get_out, n_actions_out, flags_out, st);
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout_distances launch");
   return CRAFT_OK;
@@ -863,7 +997,7 @@ int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
   if (4 * s->view.C > 1000)
     return fail(s, CRAFT_EINVAL, "craft_teacher: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
   if (n == 0) return CRAFT_OK;
-  hipError_t e = craft::launch_teacher(craft::teach_words(s->view.W, s->view.H), s->view, slots, tasks, n, action_out,
+  hipError_t e = craft::launch_teacher(craft::teach_words(s->view.W, s->view.H), s->teach_lanes, teach_view(s), slots, tasks, n, action_out,
                                        path_len_out, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_teacher launch");
   return CRAFT_OK;

@@ -520,9 +520,42 @@ __device__ __forceinline__ int tt_slot_of(const SimView& v, int kind) {
 __device__ __forceinline__ uint16_t tt_encode(bool ok, int fa, int len) {
   return (uint16_t)(0x8000u | (ok ? 0x4000u : 0u) | ((uint32_t)(fa + 1) << 10) | (uint32_t)(len + 1));
 }
-// The table row block of scenario `scen` (null when there is no table).
-__device__ __forceinline__ const uint16_t* tt_row(const SimView& v, int scen) {
-  return v.ttab ? v.ttab + (size_t)scen * v.tt_slots * 4 * v.C : nullptr;
+// The table block of table row trow = pool row * tt_nsub + subset (null when there is no table).
+__device__ __forceinline__ const uint16_t* tt_row(const SimView& v, int trow) {
+  return v.ttab ? v.ttab + (size_t)trow * v.tt_slots * 4 * v.C : nullptr;
+}
+// The table row of an env of pool row `scen` that has cleared `ncl` cells this episode, cleared(c)
+// telling which: scen * tt_nsub + the subset of the row's listed clearable cells it cleared (w0,
+// w1 = tt_cells[scen]), or -1 when it cleared a cell the table does not list (or there is no
+// table).  Every grid an env can reach is its pool row minus some of the row's clearable cells
+// (grab, bridge and axe only ever clear a cell, craft.py:383-410).
+template <class Cleared>
+__device__ __forceinline__ int tt_index(const SimView& v, int scen, uint32_t w0, uint32_t w1, int ncl,
+                                        Cleared cleared) {
+  if (!v.ttab) return -1;
+  int sub = 0, hit = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t c = ((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 0xffu;
+    if (c != 0xffu && cleared((int)c)) {
+      sub |= 1 << j;
+      ++hit;
+    }
+  }
+  return hit == ncl ? scen * v.tt_nsub + sub : -1;
+}
+// tt_index over a cleared-cell mask m (8 words, 256 cells).
+__device__ __forceinline__ int tt_index_mask(const SimView& v, int scen, uint32_t w0, uint32_t w1,
+                                             const uint32_t (&m)[8]) {
+  int ncl = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ncl += __popc(m[i]);
+  return tt_index(v, scen, w0, w1, ncl, [&](int c) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w = (i == (c >> 5)) ? m[i] : w;
+    return ((w >> (c & 31)) & 1u) != 0;
+  });
 }
 
 // DemonstrationTeacher.__call__ (teachers/demonstration.py:9-30) for one env, LANES
@@ -548,6 +581,49 @@ __device__ __forceinline__ int go_leaf_action(bool ok, int fa, int len, int& err
 // DEFER (the fused kernels; no want_len): no BFS here at all.  A go[X] leaf the table cannot
 // answer returns kTeachDeferred with *defer = X, for a later dense pass (teach_deferred).
 constexpr int kTeachDeferred = -3;
+
+// The hint-tree half of DemonstrationTeacher.__call__ alone (the K-tick teacher rollout,
+// craft_rollout_teach.h, resolves go[X] leaves later, from the table or a BFS job):
+// find_incomplete_subtask (teachers/base.py:10-25) from `task` with satisfies() read off the
+// inventory iv and the facing cell's kind.  Returns CRAFT_STOP when the task is already
+// satisfied (demonstration.py:12-13), CRAFT_USE for a use leaf, kTeachGo with go_kind = X for a
+// go[X] leaf, or -2 with err = CRAFT_ETEACHER where the reference raises (base.py:24's assert,
+// demonstration.py:18's).  The same decisions as teach_env's walk.
+constexpr int kTeachGo = -4;
+__device__ __forceinline__ int hint_leaf(const uint16_t* task_tab, const int32_t* task_sub, const uint8_t* iv,
+                                         int facing, int task, int& err, int& go_kind) {
+  auto sat = [&](int t) -> int {       // satisfies(), craft.py:285-294
+    const uint32_t tt = task_tab[t];
+    const int goal = tt & 0xf, arg = (tt >> 4) & 0xff;
+    if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) return iv[arg] > 0;
+    if (goal == CRAFT_GOAL_GO) return facing == arg;
+    return -1;
+  };
+  err = 0;
+  go_kind = -1;
+  if (sat(task) == 1) return CRAFT_STOP;
+  int node = task;
+  for (int guard = 0; guard < CRAFT_MAX_TASKS; ++guard) {
+    const int nsub = (task_tab[node] >> 12) & 0xf;
+    if (nsub == 0) break;
+    const int32_t* sub = task_sub + CRAFT_MAX_SUBTASKS * node;
+    int chosen = sub[nsub - 1];
+    bool last = true;
+    for (int q = 0; q + 1 < nsub; ++q)
+      if (sat(sub[q]) != 1) { chosen = sub[q]; last = false; break; }
+    if (last && sat(chosen) == 1) { err = CRAFT_ETEACHER; return -2; }   // base.py:24 assert
+    node = chosen;
+  }
+  const uint32_t lt = task_tab[node];
+  const int goal = lt & 0xf;
+  if (goal == CRAFT_GOAL_USE) return CRAFT_USE;
+  if (goal == CRAFT_GOAL_GO) {
+    go_kind = (lt >> 4) & 0xff;
+    return kTeachGo;
+  }
+  err = CRAFT_ETEACHER;                                                  // demonstration.py:18
+  return -2;
+}
 
 template <int NW, int LANES, bool DEFER = false>
 __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_tab, const int32_t* task_sub,

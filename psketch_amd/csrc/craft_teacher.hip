@@ -71,11 +71,13 @@ __device__ __forceinline__ int teach_item(const SimView& v, const TeachArgs& a, 
   }
   const uint8_t* iv = reinterpret_cast<const uint8_t*>(v.inv + 2 * slot);
   const uint32_t* row32 = reinterpret_cast<const uint32_t*>(v.pool + (size_t)s.scen * v.CS);
-  const bool pristine = (m[0] | m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7]) == 0u;
+  // the teacher table's row for this grid (the pool row minus the cells it cleared), if it has one
+  const int trow = v.ttab ? tt_index_mask(v, s.scen, v.tt_cells[2 * (size_t)s.scen], v.tt_cells[2 * (size_t)s.scen + 1], m)
+                          : -1;
   int len = -1, err = 0, defer = -1;
   const int action = teach_env<NW, LANES, DEFER>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
                                                  len, err, v.pool_conn[s.scen] != 0,
-                                                 pristine ? tt_row(v, s.scen) : nullptr, &defer);
+                                                 trow >= 0 ? tt_row(v, trow) : nullptr, &defer);
   if (DEFER && action == kTeachDeferred) return defer;
   if (lead) {
     if (err) latch_error(v.err, err, slot);
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
     } else {
       const int C = v.C, nq = (C + 3) >> 2;
       const int kind = (tt >> 4) & 0xffu, slot = v.ttab ? tt_slot_of(v, kind) : -1;
-      const uint32_t e = slot >= 0 ? tt_row(v, s.scen)[(slot * 4 + s.dir) * C + s.x * v.H + s.y] : 0u;
+      const uint32_t e = slot >= 0 ? tt_row(v, s.scen * v.tt_nsub)[(slot * 4 + s.dir) * C + s.x * v.H + s.y] : 0u;
       int fa = -1, len = -1;
       bool ok;
       if (e & 0x8000u) {                 // the initial grid is the pool row: the teacher table's
@@ -236,37 +238,77 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
   }
 }
 
-// ---- the teacher table (craft_teach.h): bfs_closest on the pristine grid of pool rows
-// [first, first + count) for every target-kind slot, direction and free interior start cell,
-// LANES lanes per key.  Occupied and border cells get 0 (never read: an agent stands on a free
-// interior cell, and a pristine grid is the row itself). ------------------------------------------
+// ---- the teacher table (craft_teach.h): bfs_closest for every grid an env of pool rows
+// [first, first + count) can reach -- the row with any subset of its first tt_m clearable cells
+// cleared -- for every target-kind slot, direction and free interior start cell, LANES lanes per
+// key.  Keys no env reaches get 0 (never read): occupied and border start cells, and subsets naming
+// a cell the row does not have. ---------------------------------------------------------------------
 struct TableArgs {
   int32_t first, count;
   int32_t kinds[16];         // slot -> target kind
 };
 
+// Each row's clearable cells (a kind grab, bridge or axe can clear: craft.py:383-410) in x-major
+// order, the first tt_m of them, one byte each in tt_cells[row][2] (0xff = none).
+__global__ __launch_bounds__(256) void tt_cells_kernel(SimView v, TableArgs a) {
+  const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (r >= a.count) return;
+  const int row = a.first + r;
+  const uint8_t* g = v.pool + (size_t)row * v.CS;
+  const int m = 31 - __clz((unsigned)v.tt_nsub);                         // tt_m (tt_nsub = 1 << tt_m)
+  uint32_t w[2] = {0xffffffffu, 0xffffffffu};
+  int j = 0;
+  for (int c = 0; c < v.C && j < m; ++c) {
+    const int k = g[c], cls = kind_class(v, k);
+    if (k != 0 && (cls == CRAFT_KIND_GRABBABLE || cls == CRAFT_KIND_WATER || cls == CRAFT_KIND_STONE)) {
+      w[j >> 2] = (w[j >> 2] & ~(0xffu << (8 * (j & 3)))) | ((uint32_t)c << (8 * (j & 3)));
+      ++j;
+    }
+  }
+  uint32_t* out = const_cast<uint32_t*>(v.tt_cells) + 2 * (size_t)row;
+  out[0] = w[0];
+  out[1] = w[1];
+}
+
 template <int NW, int LANES>
 __global__ __launch_bounds__(256) void teach_table_kernel(SimView v, TableArgs a) {
   const int C = v.C, H = v.H, S = v.tt_slots;
-  const int64_t per_row = (int64_t)S * 4 * C;
+  const int64_t per_sub = (int64_t)S * 4 * C, per_row = (int64_t)v.tt_nsub * per_sub;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LANES;
   const int ql = (int)(threadIdx.x % LANES);
   if (i >= (int64_t)a.count * per_row) return;          // lane-group-uniform
   const int r = (int)(i / per_row);
-  const int k = (int)(i - (int64_t)r * per_row);
-  const int slot = k / (4 * C), dir = (k / C) & 3, cell = k % C;
+  const int64_t k = i - (int64_t)r * per_row;
+  const int sub = (int)(k / per_sub);
+  const int k2 = (int)(k - (int64_t)sub * per_sub);
+  const int slot = k2 / (4 * C), dir = (k2 / C) & 3, cell = k2 % C;
   const int row = a.first + r;
   const uint8_t* g = v.pool + (size_t)row * v.CS;
+  const uint32_t cw[2] = {v.tt_cells[2 * (size_t)row], v.tt_cells[2 * (size_t)row + 1]};
+  uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};              // the subset's cleared cells
+  bool valid = true, here = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if ((sub >> j) & 1) {
+      const uint32_t c = (cw[j >> 2] >> (8 * (j & 3))) & 0xffu;
+      if (c == 0xffu) valid = false;
+      else {
+        mask_set(m, (int)c);
+        here = here || (int)c == cell;
+      }
+    }
   const int x = cell / H, y = cell - x * H;
   uint16_t e = 0;
-  if (x >= 1 && x <= v.W - 2 && y >= 1 && y <= H - 2 && g[cell] == 0) {
-    const uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const Bits<NW> valid = brange<NW>(0, C - 2 * H);
+  if (valid && x >= 1 && x <= v.W - 2 && y >= 1 && y <= H - 2 && (g[cell] == 0 || here)) {
+    const Bits<NW> vb = brange<NW>(0, C - 2 * H);
     Bits<NW> occ, tgt;
     band_bits<NW, LANES>(reinterpret_cast<const uint32_t*>(g), (C + 3) >> 2, C, H, m, (uint32_t)a.kinds[slot], ql,
                          occ, tgt);
     int fa = -1, len = -1;
-    const bool ok = bfs_closest<NW, LANES>(occ, tgt, valid, H, cell - H, dir, ql, fa, len, true, v.pool_conn[row] != 0);
+    // the row's free cells are one component (pool_conn); a subset grid may not be (its cleared
+    // cells need not border a free one), so those run the exact flood instead of the shortcut
+    const bool conn = sub == 0 && v.pool_conn[row] != 0;
+    const bool ok = bfs_closest<NW, LANES>(occ, tgt, vb, H, cell - H, dir, ql, fa, len, true, conn);
     e = tt_encode(ok, fa, len);
   }
   if (ql == 0) const_cast<uint16_t*>(v.ttab)[(size_t)row * per_row + k] = e;
@@ -279,10 +321,12 @@ hipError_t launch_teach_table(int nw, const SimView& v, int32_t first, int32_t c
   a.first = first;
   a.count = count;
   for (int s = 0; s < v.tt_slots && s < 16; ++s) a.kinds[s] = kinds[s];
+  hipLaunchKernelGGL(tt_cells_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, v, a);
   constexpr int LANES = 2;
-  const int64_t items = (int64_t)count * v.tt_slots * 4 * v.C;
-  const unsigned blocks = (unsigned)((LANES * items + 255) / 256);
-#define CRAFT_TT(NWV) hipLaunchKernelGGL((teach_table_kernel<NWV, LANES>), dim3(blocks), dim3(256), 0, st, v, a)
+  const int64_t items = (int64_t)count * v.tt_nsub * v.tt_slots * 4 * v.C;
+  const int64_t blocks = (LANES * items + 255) / 256;
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+#define CRAFT_TT(NWV) hipLaunchKernelGGL((teach_table_kernel<NWV, LANES>), dim3((unsigned)blocks), dim3(256), 0, st, v, a)
   if (nw <= 2) CRAFT_TT(2);
   else if (nw <= 4) CRAFT_TT(4);
   else if (nw <= 5) CRAFT_TT(5);
@@ -310,17 +354,14 @@ hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, cons
   return hipGetLastError();
 }
 
-hipError_t launch_teacher(int nw, const SimView& v, const int32_t* slots, const int32_t* tasks,
+hipError_t launch_teacher(int nw, int forced, const SimView& v, const int32_t* slots, const int32_t* tasks,
                           int64_t n, int32_t* act_out, int32_t* len_out, hipStream_t st) {
   TeachArgs a{slots, tasks, n, act_out, len_out};
   // nw = 32-bit words per BFS cell set (craft_teach.h: the band of columns 1 .. W-2):
   // 8x8 -> 2, 10x10 -> 3 (run as 4), 12x12 -> 4, 16x16 -> 7 (run as 8)
-  static const int forced = [] {                  // CRAFT_TEACHER_LANES=1/2/4: diagnostic override
-    const char* e = getenv("CRAFT_TEACHER_LANES");
-    const int x = e ? atoi(e) : 0;
-    return (x == 1 || x == 2 || x == 4) ? x : 0;
-  }();
-  const int lanes = forced ? forced : (n <= kTeacherQuadMaxItems ? 4 : 2);
+  // forced: craft_sim_tune_teach's lanes per query (1, 2 or 4), else 0: quads for small batches,
+  // pairs above
+  const int lanes = (forced == 1 || forced == 2 || forced == 4) ? forced : (n <= kTeacherQuadMaxItems ? 4 : 2);
   const unsigned blocks = (unsigned)((lanes * n + 255) / 256);
   // without path lengths the table's answers finish in the walk and the rest run densely
 #define CRAFT_TEACH_D(NWV, D)                                                                             \

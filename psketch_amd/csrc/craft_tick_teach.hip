@@ -15,12 +15,9 @@ static hipError_t launch_tt(const SimView& v, const TileArgs& a, size_t lds, hip
   constexpr int TILE = kMaxTileEnvs;
   const int64_t tiles = (a.n + TILE - 1) / TILE;
   if (tiles == 0) return hipSuccess;
-  if (lds > 65536) {       // 5x5 / 7x7 windows: 64-env rows past 64 KiB (gfx950 allows 160 KiB)
-    if (lds > 163840) return hipErrorInvalidValue;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<WIN, MODE_TICK, TILE, TL, NW>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
+  // 5x5 / 7x7 windows: 64-env rows past 64 KiB
+  const hipError_t e = ensure_lds<&tile_kernel<WIN, MODE_TICK, TILE, TL, NW>>(lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((tile_kernel<WIN, MODE_TICK, TILE, TL, NW>), dim3((unsigned)tiles),
                      dim3(kThreads + TILE * TL), lds, st, v, a);
   return hipGetLastError();
@@ -71,12 +68,9 @@ static hipError_t launch_t2(const SimView& v, const TileArgs& a, size_t lds, hip
   const int64_t per = (int64_t)kTick2Tiles * kTick2Tile;
   const int64_t blocks = (a.n + per - 1) / per;
   if (blocks == 0) return hipSuccess;
-  if (lds > 65536) {       // the teacher waves' own rows (tick2_share) pass 64 KiB
-    if (lds > 163840) return hipErrorInvalidValue;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tick2_kernel<3, kTick2Tiles, TW, TL, NW>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
+  // the teacher waves' own rows (tick2_share) pass 64 KiB
+  const hipError_t e = ensure_lds<&tick2_kernel<3, kTick2Tiles, TW, TL, NW>>(lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((tick2_kernel<3, kTick2Tiles, TW, TL, NW>), dim3((unsigned)blocks),
                      dim3(64 * TW + kTick2Tiles * kTick2Tile * TL), lds, st, v, a);
   return hipGetLastError();

@@ -147,8 +147,14 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
       }
     }
     uint8_t* g = s_grid + tid * v.GS;
-    uint32_t conn = 0;                                     // TL > 0: the scenario's free cells connected
-    if (TL > 0 && live) conn = v.pool_conn[s.scen];
+    uint32_t conn = 0, tcw0 = ~0u, tcw1 = ~0u;           // TL > 0: the scenario's free cells connected,
+    if (TL > 0 && live) {                                  // its clearable cells the teacher table lists
+      conn = v.pool_conn[s.scen];
+      if (v.ttab) {
+        tcw0 = v.tt_cells[2 * (size_t)s.scen];
+        tcw1 = v.tt_cells[2 * (size_t)s.scen + 1];
+      }
+    }
     if (live) {
       // the env's scenario grid: CS/16 independent 16-byte loads (L2-resident pool)
       const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
@@ -280,13 +286,16 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
     }
     if ((MODE == MODE_TICK || MODE == MODE_TRANSITION) && a.code && tid < nE) a.code[env0 + tid] = (int8_t)code;
     s_agent[tid] = live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24)) : 0u;
-    // the teacher's inputs: task | frozen << 8 | scenario connected << 9 | grid pristine (no cell
-    // cleared: the teacher table answers, craft_teach.h) << 10 | scenario << 11 (< 2^21 when the
-    // table is on)
-    if (TL > 0)
+    // the teacher's inputs: task | frozen << 8 | scenario connected << 9 | the teacher table has
+    // this grid (craft_teach.h) << 10 | its table row << 11 (< 2^21 when the table is on)
+    if (TL > 0) {
+      int ncl = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) ncl += __popc(m[w]);
+      const int trow = live ? tt_index(v, s.scen, tcw0, tcw1, ncl, [&](int c) { return g[c] == 0; }) : -1;
       s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9) |
-                      ((m[0] | m[1] | m[2] | m[3] | m[4] | m[5] | m[6] | m[7]) == 0u ? 1u << 10 : 0u) |
-                      ((uint32_t)s.scen << 11);
+                     (trow >= 0 ? (1u << 10) | ((uint32_t)trow << 11) : 0u);
+    }
     if (MODE == MODE_TICK) {
       // episode statistics: one partial-sum row per workgroup (uncontended)
       const uint64_t bs = __ballot(live && counted && d && succ == 1);

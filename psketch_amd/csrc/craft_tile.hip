@@ -8,12 +8,9 @@ template <int WIN, int MODE, int TILE>
 static hipError_t launch_one(const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
   const int64_t tiles = (a.n + TILE - 1) / TILE;
   if (tiles == 0) return hipSuccess;
-  if (lds > 65536) {       // u8 rows of 5x5 / 7x7 windows on large tiles (gfx950 allows 160 KiB)
-    if (lds > 163840) return hipErrorInvalidValue;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&tile_kernel<WIN, MODE, TILE>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
+  // u8 rows of 5x5 / 7x7 windows on large tiles
+  const hipError_t e = ensure_lds<&tile_kernel<WIN, MODE, TILE>>(lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((tile_kernel<WIN, MODE, TILE>), dim3((unsigned)tiles), dim3(kThreads), lds, st, v, a);
   return hipGetLastError();
 }

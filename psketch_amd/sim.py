@@ -69,10 +69,12 @@ class CraftSim:
         self._h = handle
         self.obs_format, self.obs_dtype = "f32", torch.float32
         self._rollout_cache = None
+        self._teach_cache = None
 
     # ---- lifetime ---------------------------------------------------------------
     def close(self):
         self._rollout_cache = None
+        self._teach_cache = None
         if getattr(self, "_h", None):
             self._L.craft_sim_destroy(self._h)
             self._h = None
@@ -97,11 +99,14 @@ class CraftSim:
         self._check(self._L.craft_sim_tune_rollout(self._h, int(chunk_ticks), int(threads)),
                     "craft_sim_tune_rollout")
 
-    def tune_teach(self, kernel=0):
-        """Which kernel step(..., labels=) launches (craft_sim_tune_teach): 0 the
-        measured best, 1 the one-tile kernel, 2 the two-tile kernel (3x3 windows); results
-        are identical for every setting."""
-        self._check(self._L.craft_sim_tune_teach(self._h, int(kernel)), "craft_sim_tune_teach")
+    def tune_teach(self, kernel=0, lanes=0, table=0):
+        """The teacher's knobs (craft_sim_tune_teach; results are identical for every
+        setting): kernel = which kernel step(..., labels=) launches (0 the measured best, 1 the
+        one-tile kernel, 2 the two-tile kernel, 3x3 windows); lanes = teacher lanes per query
+        (0 default, 1, 2 or 4); table = which teachers read the teacher table (0 auto, 1 always,
+        2 never: every query runs the BFS)."""
+        self._check(self._L.craft_sim_tune_teach(self._h, int(kernel), int(lanes), int(table)),
+                    "craft_sim_tune_teach")
 
     def step_shape(self, teach=False):
         """(kernel name, envs per tile / workgroup, teacher lanes per env) that step()
@@ -120,6 +125,12 @@ class CraftSim:
                                                     ctypes.byref(sp)), "craft_sim_rollout_shape")
         return t.value, nt.value, bool(sp.value)
 
+    def teach_words(self):
+        """32-bit words per cell set of the teacher's BFS as the kernels are instantiated (the
+        band of columns 1 .. W-2: 8x8 -> 2, 10x10 and 12x12 -> 4, up to 15x15 -> 8)."""
+        nw = ((self.width - 2) * self.height + 31) // 32
+        return 2 if nw <= 2 else 4 if nw <= 4 else 8
+
     def tile_shape(self):
         """(tile_envs, obs_store) of the tick kernel (craft_sim_tile_shape)."""
         t, st = ctypes.c_int32(), ctypes.c_int32()
@@ -137,6 +148,7 @@ class CraftSim:
         self._check(self._L.craft_sim_set_obs_format(self._h, code), "craft_sim_set_obs_format")
         self.obs_format, self.obs_dtype = fmt, dtype
         self._rollout_cache = None
+        self._teach_cache = None
 
     def _stream(self):
         # the raw hipStream_t of the caller's current stream on this device (an int; the C ABI's
@@ -359,6 +371,86 @@ class CraftSim:
                 self._ring_sig(obs, reward, done, success),
                 (_ptr(obs), int(ring or 1), _ptr(reward), _ptr(done), _ptr(success)))
         return obs
+
+    def rollout_teach(self, n_ticks, seed=0, tick0=0, actions=None, autoreset=True, obs=None,
+                      reward=None, done=None, success=None, labels=None, action_record=None,
+                      label_in=None, behavior_clone=None, label_actions=False):
+        """n_ticks ticks with the DemonstrationTeacher's label of every slot's new state after
+        each one, in one launch (include/craft.h craft_rollout_teach): identical to n_ticks
+        step(..., labels=) calls.  Each tick's action per slot: its current state's label when
+        label_actions (every slot: make_data's demonstrations) or behavior_clone[i] (uint8 [N]),
+        else actions[k] (int32 [n_ticks, N]) or the hashed draw.  label_in (int32 [N]): the
+        labels of the states before tick0, needed when labels feed actions (teacher() of the
+        reset states, or the previous launch's last labels slot).  Outputs are [R, ...] rings
+        (tick t writes slot t % R): obs, reward, done, success, labels (int32), action_record
+        (int32, -1 for done slots)."""
+        n = self.n_envs
+        if n_ticks < 0:
+            raise ValueError("n_ticks must be >= 0")
+        outs_t = (obs, reward, done, success, labels, action_record)
+        if actions is None and label_in is None and behavior_clone is None and not label_actions:
+            # the same output rings as the last call (a benchmark loop): their checks still hold
+            c = self._teach_cache
+            if c is not None and c[1] == self._ring_sig(*outs_t) and all(
+                    (r is None and t is None) or (r is not None and r() is t) for r, t in zip(c[0], outs_t)):
+                args = c[2]
+                args.action_seed = seed & (2**64 - 1)
+                args.tick0 = int(tick0)
+                args.n_ticks = int(n_ticks)
+                args.flags = N.STEP_AUTORESET if autoreset else 0
+                self._check(self._L.craft_rollout_teach(self._h, ctypes.byref(args), self._stream()),
+                            "craft_rollout_teach")
+                return labels
+        args = N.craft_rollout_teach_args_t()
+        keep = []
+
+        def put(field, t):
+            if t is not None:
+                keep.append(t)
+                setattr(args, field, t.data_ptr())
+
+        ring = None
+        outs = (("obs", obs), ("reward", reward), ("done", done), ("success", success),
+                ("labels", labels), ("action_record", action_record))
+        for name, t in outs:
+            if t is not None:
+                if t.dim() < 1 or t.shape[0] < 1:
+                    raise ValueError(f"{name} must be a ring [R >= 1, {n}, ...]")
+                if ring is not None and t.shape[0] != ring:
+                    raise ValueError(f"{name} ring {t.shape[0]} != ring {ring} of the other outputs")
+                ring = t.shape[0]
+        ring = ring or 1
+        if obs is not None:
+            self._buf("obs", obs, self.obs_dtype, (ring, n, self.n_features))
+        for name, t, dt in (("reward", reward, torch.float32), ("done", done, torch.uint8),
+                            ("success", success, torch.int8), ("labels", labels, torch.int32),
+                            ("action_record", action_record, torch.int32)):
+            self._buf(name, t, dt, (ring, n) if t is not None else ())
+        for name, t in outs:
+            put(name, t)
+        if actions is not None:
+            put("actions", self._i32(actions, n * n_ticks))
+        if label_in is not None:
+            put("label_in", self._i32(label_in, n))
+        if behavior_clone is not None:
+            bc = torch.as_tensor(behavior_clone, device=self.device)
+            bc = (bc != 0).to(torch.uint8).contiguous() if bc.dtype != torch.uint8 else bc.contiguous()
+            if bc.numel() != n:
+                raise ValueError(f"behavior_clone: expected {n} entries")
+            put("behavior_clone", bc)
+        args.label_actions = 1 if label_actions else 0
+        args.action_seed = seed & (2**64 - 1)
+        args.tick0 = int(tick0)
+        args.n_ticks = int(n_ticks)
+        args.flags = N.STEP_AUTORESET if autoreset else 0
+        args.ring = int(ring)
+        self._check(self._L.craft_rollout_teach(self._h, ctypes.byref(args), self._stream()),
+                    "craft_rollout_teach")
+        if actions is None and label_in is None and behavior_clone is None and not label_actions:
+            # weak references: the cache keeps no output alive
+            self._teach_cache = (tuple(None if t is None else weakref.ref(t) for t in outs_t),
+                                 self._ring_sig(*outs_t), args)
+        return labels
 
     @staticmethod
     def _ring_sig(*ts):

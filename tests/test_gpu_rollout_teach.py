@@ -1,0 +1,221 @@
+"""craft_rollout_teach on the GPU (csrc/craft_rollout_teach.h): K ticks and the
+DemonstrationTeacher's label of every env's new state per tick in one launch.  Checked tick by
+tick against craft_step_teach (itself pinned to craft_teacher, the oracle and the reference's 4400
+demonstrations), against the CPU variant of the ABI, against the oracle on sampled global ids at
+config 5's size, and by regenerating the reference's demonstrations (make_data.py:146-152) in
+20-tick launches."""
+import numpy as np
+import pytest
+import torch
+
+from psketch_amd import CraftSim, sample_scenarios, synthetic_specs
+from tests.helpers import make_tables
+from tests.test_gpu_parity import host, set_states, sim_with_pool
+
+pytestmark = pytest.mark.gpu
+
+
+def _rings(sim, ring):
+    n, dev = sim.n_envs, sim.device
+    return dict(obs=torch.zeros((ring, n, sim.n_features), dtype=sim.obs_dtype, device=dev),
+                done=torch.zeros((ring, n), dtype=torch.uint8, device=dev),
+                success=torch.zeros((ring, n), dtype=torch.int8, device=dev),
+                reward=torch.zeros((ring, n), dtype=torch.float32, device=dev),
+                labels=torch.zeros((ring, n), dtype=torch.int32, device=dev),
+                action_record=torch.zeros((ring, n), dtype=torch.int32, device=dev))
+
+
+def _setup(world, W, n, pool_n=256, seed=6, base=0):
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, pool_n)
+    specs = synthetic_specs(pool, W, W, n, base, seed=seed, task_ids=[t.id for t in tm.dataset_tasks()])
+    return cfg, pool, specs
+
+
+# mode: policy = the hashed draw; given = an action table (USE raised: cells cleared, recipes);
+# bc = behaviour cloning on half the envs; label = every env acts on its label (demonstrations)
+@pytest.mark.parametrize("world,W,n,T,K,ring,mode,autoreset", [
+    ("craft_medium_12x12", 12, 65536, 40, 20, 40, "policy", True),   # config 5's size
+    ("craft_medium_12x12", 12, 65536, 40, 40, 8, "given", True),     # ring < K: slots rewritten
+    ("craft_medium_12x12", 12, 20000, 40, 13, 40, "bc", True),
+    ("craft_medium_12x12", 12, 5000, 40, 40, 40, "label", False),    # partial tile, frozen envs
+    ("craft_medium_12x12", 12, 4099, 30, 10, 30, "bc", False),
+    ("craft_medium", 8, 3000, 30, 15, 30, "given", True),            # 8x8: two words per cell set
+    ("craft_large", 10, 1500, 25, 25, 25, "policy", True),           # 10x10, 5x5 windows
+    ("craft_medium_12x12_w5", 12, 2048, 25, 25, 25, "given", True)])
+def test_rollout_teach_equals_step_teach(world, W, n, T, K, ring, mode, autoreset):
+    cfg, pool, specs = _setup(world, W, n)
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.reset(*specs)
+    b.reset(*specs)
+    rng = np.random.RandomState(11)
+    acts = (rng.choice(6, size=(T, n), p=[.18, .18, .18, .18, .26, .02]).astype(np.int32)
+            if mode == "given" else None)
+    bc = (rng.rand(n) < 0.5).astype(np.uint8) if mode == "bc" else None
+    src = (torch.ones(n, dtype=torch.uint8, device="cuda") if mode == "label"
+           else (torch.as_tensor(bc, device="cuda") if bc is not None else None))
+    cur = b.teacher()[0].clone()                                  # labels of the reset states
+    out = _rings(a, ring)
+    lab_in = cur.clone()
+    F = a.n_features
+    ob = torch.empty((n, F), dtype=torch.float32, device="cuda")
+    db, rb = torch.empty(n, dtype=torch.uint8, device="cuda"), torch.empty(n, dtype=torch.float32, device="cuda")
+    sb, recb = torch.empty(n, dtype=torch.int8, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda")
+    lb = torch.empty(n, dtype=torch.int32, device="cuda")
+    for t0 in range(0, T, K):
+        k = min(K, T - t0)
+        a.rollout_teach(k, seed=3, tick0=t0,
+                        actions=None if acts is None else torch.as_tensor(acts[t0:t0 + k], device="cuda"),
+                        autoreset=autoreset, label_in=lab_in if src is not None else None,
+                        behavior_clone=None if bc is None else torch.as_tensor(bc, device="cuda"),
+                        label_actions=mode == "label", **out)
+        lab_in = out["labels"][(t0 + k - 1) % ring].clone()
+        for t in range(t0, t0 + k):
+            b.step(None if acts is None else torch.as_tensor(acts[t], device="cuda"), seed=3, tick=t,
+                   autoreset=autoreset, obs=ob, reward=rb, done=db, success=sb, action_record=recb,
+                   ref_actions=cur if src is not None else None, behavior_clone=src, labels=lb)
+            cur = lb.clone()
+            if t >= T - ring or ring >= T:                       # slots not rewritten later
+                r = t % ring
+                assert torch.equal(out["obs"][r], ob), t
+                for key, ref in (("done", db), ("success", sb), ("reward", rb), ("action_record", recb),
+                                 ("labels", lb)):
+                    assert torch.equal(out[key][r], ref), (key, t)
+    sa, sb2 = a.get_state(), b.get_state()
+    for key in sa:
+        assert torch.equal(sa[key], sb2[key]), key
+    np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
+    if mode == "label" and not autoreset:
+        assert bool((lb == -1).all())                             # every demonstration ended
+    a.check()
+    b.check()
+
+
+@pytest.mark.parametrize("mode", ["policy", "bc", "label"])
+def test_rollout_teach_hip_equals_cpu_variant(mode):
+    world, W, n, T = "craft_medium_12x12", 12, 2048, 35
+    cfg, pool, specs = _setup(world, W, n, seed=2)
+    g = sim_with_pool(world, n, pool)
+    c = CraftSim(world, n_envs=n, device="cpu", pool_capacity=len(pool))
+    c.load_pool(pool)
+    g.reset(*specs)
+    c.reset(*specs)
+    bc = (np.random.RandomState(4).rand(n) < 0.5).astype(np.uint8)
+    kw = {}
+    if mode == "bc":
+        kw = dict(behavior_clone=bc)
+    elif mode == "label":
+        kw = dict(label_actions=True)
+    outs = []
+    for s in (g, c):
+        r = _rings(s, T)
+        if mode != "policy":
+            kw["label_in"] = s.teacher()[0].clone()
+        s.rollout_teach(T, seed=9, autoreset=mode != "label", **{k: (torch.as_tensor(v, device=s.device)
+                                                                    if isinstance(v, np.ndarray) else v)
+                                                                 for k, v in kw.items()}, **r)
+        s.check()
+        outs.append({k: v.cpu() for k, v in r.items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_rollout_teach_vs_oracle_full_size(oracle_mod):
+    """Config 5's launch (65,536 envs, 40 ticks of hashed actions with auto-reset, every env
+    labelled every tick) against the literal oracle on 256 sampled global ids, run from their
+    initial states with their own ids."""
+    from oracle import rollout_oracle
+    world, W, n, T, base = "craft_medium_12x12", 12, 65536, 40, 65536
+    cfg, pool, specs = _setup(world, W, n, pool_n=1024, seed=0, base=base)
+    sim = sim_with_pool(world, n, pool, env_id_base=base)
+    sim.reset(*specs)
+    out = _rings(sim, T)
+    sim.rollout_teach(20, seed=5, tick0=0, **out)
+    sim.rollout_teach(20, seed=5, tick0=20, **out)
+    sim.check()
+    pick = np.sort(np.random.RandomState(1).choice(n, 256, replace=False))
+    o = oracle_mod.Oracle(cfg, pool)
+    envs = o.init_envs(*[np.asarray(x)[pick] for x in specs])
+    ref = rollout_oracle.teach_rollout(o, envs, base + pick, T, seed=5)
+    for k in ("labels", "action_record", "done", "success"):
+        np.testing.assert_array_equal(host(out[k])[:, pick], ref[k], err_msg=k)
+    assert (ref["labels"] >= 0).mean() > 0.9
+
+
+@pytest.mark.parametrize("split", ["dev", "test"])
+def test_demonstrations_regenerated_on_gpu(golden, split):
+    """make_data.get_reference_actions (make_data.py:146-152) for every committed instance, on
+    the GPU in 20-tick launches: every env acts on its label until STOP.  The action record is
+    the reference's ref_actions and every episode ends satisfied."""
+    g = golden("devtest.npz")
+    n = len(g[f"{split}_task"])
+    sim = sim_with_pool("craft_medium", n, g[f"{split}_grids"])
+    pos = g[f"{split}_pos"].astype(np.int32)
+    agent = np.concatenate([pos, np.zeros((n, 1), np.int32)], 1)
+    set_states(sim, g[f"{split}_world"], agent, np.zeros((n, 1)), task=g[f"{split}_task"])
+    ref = g[f"{split}_actions"].astype(np.int32)
+    label_in = sim.teacher()[0].clone()
+    rec = []
+    for tick0 in (0, 20):
+        out = _rings(sim, 20)
+        sim.rollout_teach(20, tick0=tick0, label_in=label_in, label_actions=True, autoreset=False, **out)
+        rec.append(host(out["action_record"]))
+        label_in = out["labels"][19].clone()
+    sim.check()
+    rec = np.concatenate(rec)
+    L = ref.shape[1]
+    np.testing.assert_array_equal(rec[:L].T, ref)
+    assert (rec[L:] == -1).all()
+    sat = torch.empty(n, dtype=torch.int8, device="cuda")
+    sim.observe(sat=sat, n=n)
+    assert (host(sat) == 1).all()
+
+
+def test_rollout_teach_with_and_without_table():
+    """The teacher table (pristine grids answered at pool load) against every query running the
+    BFS (craft_sim_tune_teach table = 2): identical labels."""
+    world, W, n, T = "craft_medium_12x12", 12, 32768, 40
+    cfg, pool, specs = _setup(world, W, n, seed=3)
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    b.tune_teach(0, 0, 2)
+    rng = np.random.RandomState(7)
+    acts = torch.as_tensor(rng.choice(6, size=(T, n), p=[.18, .18, .18, .18, .26, .02]).astype(np.int32),
+                           device="cuda")
+    outs = []
+    for s in (a, b):
+        s.reset(*specs)
+        r = _rings(s, T)
+        s.rollout_teach(T, actions=acts, **r)
+        s.check()
+        outs.append(r)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_rollout_teach_graph_replay():
+    """A launch captured into a HIP graph (its own zeroed work counter) replays like eager
+    launches, interleaved with them."""
+    world, W, n, K = "craft_medium_12x12", 12, 8192, 8
+    cfg, pool, specs = _setup(world, W, n, seed=5)
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.reset(*specs)
+    b.reset(*specs)
+    ra, rb = _rings(a, K), _rings(b, K)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        a.rollout_teach(K, seed=1, tick0=0, **ra)                # warm (eager)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        a.rollout_teach(K, seed=1, tick0=K, **ra)
+    b.rollout_teach(K, seed=1, tick0=0, **rb)
+    for rep in range(3):
+        g.replay()                                                # ticks K..2K-1 each time (same tick0)
+        torch.cuda.synchronize()
+        b.rollout_teach(K, seed=1, tick0=K, **rb)
+        for k in ra:
+            assert torch.equal(ra[k], rb[k]), (k, rep)
+        a.rollout_teach(K, seed=1, tick0=0, **ra)                # eager between replays
+        b.rollout_teach(K, seed=1, tick0=0, **rb)
+    a.check()
+    b.check()

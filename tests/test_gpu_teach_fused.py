@@ -97,3 +97,49 @@ def test_step_teach_rejects_oversized_worlds():
     lab = torch.empty(64, dtype=torch.int32, device="cuda")
     with pytest.raises(N.CraftError):
         sim.step(seed=0, tick=0, labels=lab)
+
+
+@pytest.mark.parametrize("table,obs_mode", [(0, "reused"), (0, "null"), (2, "ring")])
+def test_step_teach_late_episode_vs_oracle(oracle_mod, table, obs_mode):
+    """A whole 40-tick episode at config 5's size with USE raised, so cleared cells and crafted
+    inventories are common late in the episode, and 1024 envs checked against the literal BFS
+    oracle at ticks 9, 25 and 38 (teachers/base.py:10-87): with the teacher table read (auto mode
+    reads it when obs is NULL or one buffer is rewritten every tick) and with it off (table 2),
+    observations going to a fresh ring slot every tick."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 512)
+    n = 65536
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=12, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    sim.tune_teach(0, 0, table)
+    sim.reset(*specs)
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    F = sim.n_features
+    ring = [torch.empty((n, F), dtype=torch.float32, device="cuda") for _ in range(2 if obs_mode == "ring" else 1)]
+    rng = np.random.RandomState(21)
+    o = oracle_mod.Oracle(cfg, pool)
+    pick = np.random.RandomState(4).choice(n, 1024, replace=False)
+    checked = 0
+    for t in range(40):
+        acts = torch.as_tensor(rng.choice(6, size=n, p=[.15, .15, .15, .15, .38, .02]).astype(np.int32),
+                               device="cuda")
+        obs = None if obs_mode == "null" else ring[t % len(ring)]
+        sim.step(acts, seed=5, tick=t, autoreset=False, obs=obs, labels=lab)
+        if t in (9, 25, 38):
+            st = {k: host(v) for k, v in sim.get_state().items()}
+            sim.check()
+            lh = host(lab)
+            cleared = (st["grid"][pick] != pool[st["spec"][pick, 0]]).any(1)
+            crafted = st["inventory"][pick][:, 12:].sum(1) > 0           # planks and later products
+            if t >= 25:
+                assert cleared.mean() > 0.2 and crafted.any(), (t, cleared.mean())
+            for i in pick:
+                x, y, d, _ = st["agent"][i]
+                if lh[i] == -1:                                          # frozen: the episode ended
+                    continue
+                env = o.env(st["grid"][i], x, y, d, st["inventory"][i])
+                rc, act = o.teacher(env, int(specs[4][i]))
+                assert (rc == 0 and act == lh[i]) or (rc != 0 and lh[i] == -2), (t, i)
+                checked += 1
+    assert checked > 1024

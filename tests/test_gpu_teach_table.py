@@ -1,8 +1,8 @@
 """The teacher table (craft_teach.h): find_closest_resources answered ahead of time for every
 pool row's pristine grid, read by every teacher query whose env has cleared no cell.  It is the
 same function evaluated earlier, so every label, path length and summary must equal the BFS's
-(CRAFT_TEACH_TABLE=0 at creation turns the table off; CRAFT_TT_FUSED=0 keeps the fused tick +
-teacher kernels off it, which these tests set to 1, the default, explicitly).  The reference fixtures of
+(craft_sim_tune_teach(.., table=2) keeps every teacher off the table; table=1 makes the fused tick +
+teacher kernels read it on every launch, which these tests set explicitly).  The reference fixtures of
 tests/test_gpu_parity.py (teacher_12x12.npz with its raising calls, the 4400 demonstrations) run
 through the table path too: their states are set with set_state, i.e. pristine grids."""
 import numpy as np
@@ -15,16 +15,14 @@ from tests.helpers import make_tables, world_for
 pytestmark = pytest.mark.gpu
 
 
-def _pair(monkeypatch, world, n, pool):
+def _pair(world, n, pool, kernel=0):
+    """Two simulators: every teacher on the table (table=1), and none (table=2)."""
     out = []
-    monkeypatch.setenv("CRAFT_TT_FUSED", "1")             # the fused kernels read the table (default)
-    for flag in ("1", "0"):
-        monkeypatch.setenv("CRAFT_TEACH_TABLE", flag)
+    for table in (1, 2):
         s = CraftSim(world, n_envs=n, device=0, pool_capacity=len(pool))
         s.load_pool(pool)
+        s.tune_teach(kernel, 0, table)
         out.append(s)
-    monkeypatch.delenv("CRAFT_TEACH_TABLE")
-    monkeypatch.delenv("CRAFT_TT_FUSED")
     return out
 
 
@@ -33,15 +31,14 @@ def _pair(monkeypatch, world, n, pool):
                                                     ("craft_medium_12x12_w5", 12, 5000, 0),
                                                     ("craft_medium", 8, 4096, 0),
                                                     ("craft_16x16_w7", 16, 2000, 0)])
-def test_step_teach_labels_with_and_without_table(monkeypatch, world, W, n, teach_kernel):
+def test_step_teach_labels_with_and_without_table(world, W, n, teach_kernel):
     params, cb, tm, cfg = make_tables(world)
     if 4 * W * W > 1000:
         pytest.skip("4*W*H > 1000: no teacher (teachers/base.py:42)")
     pool, _, _ = sample_scenarios(params, cb, 123, 128)
     specs = synthetic_specs(pool, W, W, n, 0, seed=9, task_ids=[t.id for t in tm.dataset_tasks()])
-    a, b = _pair(monkeypatch, world, n, pool)
+    a, b = _pair(world, n, pool, teach_kernel)
     for s in (a, b):
-        s.tune_teach(teach_kernel)
         s.reset(*specs)
     rng = np.random.RandomState(n)
     labels = [torch.empty(n, dtype=torch.int32, device="cuda") for _ in range(2)]
@@ -61,7 +58,7 @@ def test_step_teach_labels_with_and_without_table(monkeypatch, world, W, n, teac
     b.check()
 
 
-def test_rollout_summary_with_and_without_table(monkeypatch):
+def test_rollout_summary_with_and_without_table():
     """craft_rollout_distances always searches the initial (pool) grid: with the table it never
     runs the BFS; distances, is_get and the raise flags are the BFS's."""
     from psketch_amd.rollout import do_rollout
@@ -70,7 +67,7 @@ def test_rollout_summary_with_and_without_table(monkeypatch):
     pool, _, _ = sample_scenarios(params, cb, 123, 256)
     n = 20000
     spec = synthetic_specs(pool, 12, 12, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
-    a, b = _pair(monkeypatch, world, n, pool)
+    a, b = _pair(world, n, pool)
     W = torch.as_tensor(np.random.RandomState(3).randint(-3, 4, size=(cfg.n_features, 6)), dtype=torch.float32,
                         device="cuda")
 
