@@ -51,6 +51,9 @@ namespace craft {
 constexpr int kRtThreads = 512;        // C, D, 5 streaming waves, the teacher
 constexpr int kRtRows = 8;             // label rows in flight: item g -> row g & 7
 constexpr int kRtQueue = 32;           // BFS jobs waiting for a quad
+// Table answers are fetched kRtLag walks ahead of their decode: a load from the table (hundreds of
+// MB, random rows) takes longer than an interval while the store stream saturates HBM.
+constexpr int kRtLag = 4;
 // label row control word: 0 free; kRowFill | pending labels while the teacher fills it (== kRowFill:
 // complete); kRowStoring while wave 2 copies it out
 constexpr uint32_t kRowFill = 1u << 30, kRowStoring = 1u << 29;
@@ -61,9 +64,10 @@ constexpr uint32_t kRtSpinCap = 1u << 22;
 // LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation rows [2][up16(TILE*F)] |
 // inventory rows [2][TILE][36] | agent words [2][TILE] | teacher info words [2][TILE] | task table
 // [64] u16 | subtasks [64][4] | recipe words [16][3] | control words [8] | label rows
-// [8][4 + TILE] | BFS job queue [32][2 NW + 1] | table requests [2][TILE] | clearable cells [TILE][2]
+// [8][4 + TILE] | BFS job queue [32][2 NW + 1] | table requests [4][TILE] | table words [4][64] |
+// their rows [4] | clearable cells [TILE][2]
 struct RtLds {
-  int pristine, obs, inv, agent, tinfo, task, tsub, rc, ctrl, rows, jobs, treq, tcell, bytes;
+  int pristine, obs, inv, agent, tinfo, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, bytes;
 };
 __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -79,8 +83,10 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.ctrl = l.rc + CRAFT_MAX_RECIPES * 12;
   l.rows = up16(l.ctrl + 32);
   l.jobs = up16(l.rows + kRtRows * (4 + tile) * 4);
-  l.treq = up16(l.jobs + kRtQueue * (2 * NW + 1) * 4);   // [2][tile] table-entry requests
-  l.tcell = l.treq + 2 * tile * 4;                         // [tile][2] each env's listed clearable cells
+  l.treq = up16(l.jobs + kRtQueue * (2 * NW + 1) * 4);   // [kRtLag][tile] table-entry requests
+  l.tval = l.treq + kRtLag * tile * 4;                     // [kRtLag][64] the words fetched (LDS-DMA)
+  l.tpend = l.tval + kRtLag * 64 * 4;                      // [kRtLag] their label rows (~0: none)
+  l.tcell = l.tpend + kRtLag * 4;                          // [tile][2] each env's listed clearable cells
   l.bytes = up16(l.tcell + tile * 8);
   return l;
 }
@@ -140,14 +146,15 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   // [2][TILE] x | y<<8 | dir<<16 | live<<24 | frozen<<25 | cells cleared this episode (63 = more) << 26
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
   uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.tinfo);  // [2][TILE] task|conn<<8|scen<<10
-  uint32_t* s_treq = reinterpret_cast<uint32_t*>(smem + lay.treq);    // [2][TILE] ttab index, ~0 = none
+  uint32_t* s_treq = reinterpret_cast<uint32_t*>(smem + lay.treq);    // [kRtLag][TILE] ttab index, ~0 = none
+  uint32_t* s_tval = reinterpret_cast<uint32_t*>(smem + lay.tval);    // [kRtLag][64] fetched table words
+  uint32_t* s_tpend = reinterpret_cast<uint32_t*>(smem + lay.tpend);  // [kRtLag] their label rows, ~0 none
   uint32_t* s_tcell = reinterpret_cast<uint32_t*>(smem + lay.tcell);  // [TILE][2] tt_cells of the env's row
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   // [0] the claimed unit, [1] barrier arrivals, [2] items whose labels are complete (label actions),
-  // [3] 1 + the first slot whose table answer raised, [4] its status, [5 + p] the label row of the
-  // table requests of item parity p (~0: none)
+  // [3], [4] unused
   uint32_t* s_ctrl = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
   uint32_t* s_rows = reinterpret_cast<uint32_t*>(smem + lay.rows);    // [8][RW]: ctrl, tag = g + 1, tile, ring slot, labels
   uint32_t* s_jobs = reinterpret_cast<uint32_t*>(smem + lay.jobs);    // [32][JW]
@@ -170,6 +177,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   }
   if (tid < 8) s_ctrl[tid] = 0u;
   for (int i = tid; i < kRtRows * RW; i += NT) s_rows[i] = 0u;
+  if (tid < kRtLag) s_tpend[tid] = ~0u;
   __syncthreads();                                                    // (not counted: nb starts at 0)
 
   // Barriers.  Every wave adds one arrival per barrier before s_barrier; the teacher wave first
@@ -472,86 +480,33 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       gbase += nq;
     }
   } else if (wave == 1) {
-    // ======================= D: the scatter, and the teacher table's answers =====================
-    // With policy actions the teacher's walk of item i posts its table-entry requests (s_treq)
-    // and this wave loads them after its scatter of interval i + 1, then decodes them two barriers
-    // later: a load takes longer than an interval under the store stream, and a load waits only
-    // for this wave's own (it issues no store).  Exactly one load instruction per barrier and the
-    // loop unrolled by two (register sets a, b) keep the wait at vmcnt(1): the set decoded at a
-    // barrier is the one loaded two barriers before, the other stays in flight.
-    // (the 32-bit word holding the u16 entry: a u16 load's zero-extension made the compiler wait
-    // for it right after the load's barrier)
-    const uint32_t* tbase = reinterpret_cast<const uint32_t*>(v.ttab ? v.ttab : v.task_tab);
-    int bk = kBClaim, i = 0, nq = 0, nE = 0;
-    uint32_t u = 0;
-    uint32_t va = 0, vb = 0;                                           // table words in flight
-    int ra = -1, rb = -1;                                              // their label rows (-1: none)
-    int na = 0, nb2 = 0;                                               // 0 no request, 1 low half, 2 high
-    auto decode = [&](uint32_t word, int row, int need) __attribute__((always_inline)) {
-      uint32_t* R = s_rows + row * RW;
-      const uint32_t val = need == 2 ? word >> 16 : word & 0xffffu;
-      if (need) {
-        int err = 0, label = -2;
-        if (val & 0x8000u) label = go_leaf_action((val & 0x4000u) != 0, (int)((val >> 10) & 7u) - 1,
-                                                  (int)(val & 0x3ffu) - 1, err);
-        else err = CRAFT_EINVARIANT;                                   // (a reachable grid has its entry)
-        R[4 + lane] = (uint32_t)label;
-        if (err) {                                                     // latched at the end (no VMEM here)
-          uint32_t exp = 0u;
-          if (__hip_atomic_compare_exchange_strong(&s_ctrl[3], &exp, 1u + R[2] * TILE + lane, __ATOMIC_RELAXED,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-            s_ctrl[4] = (uint32_t)err;
-        }
-      }
-      const uint32_t cnt = (uint32_t)__popcll(__ballot(need != 0));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0 && cnt)
-        __hip_atomic_fetch_add(&R[0], 0u - cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    // one barrier's work with register set (val, row, need); false after the last claim
-    auto d_slot = [&](uint32_t& val, int& row, int& need) __attribute__((always_inline)) -> bool {
-      if (row >= 0) decode(val, row, need);
-      if (bk == kBTick && i < nq && want_obs) {                        // D(i)
-        const int e = lane % TILE;
-        const uint32_t ag = s_agent[(i & 1) * TILE + e];
-        if (e < nE && ((ag >> 24) & 1u))
-          scatter_env_part<WIN, P>(v, s_grid + (i & 1) * TILE * GS + e * GS,
-                                   s_inv + (i & 1) * TILE * kInvStride + e * kInvStride, ag,
-                                   s_obs + (i & 1) * obs_buf + e * F, lane / TILE);
-      }
-      row = -1;
-      uint32_t req = ~0u;
-      if (!lsync && bk == kBTick && i >= 1) {                          // item i - 1's requests
-        const uint32_t r = s_ctrl[5 + ((i - 1) & 1)];
-        if (r != ~0u) {
-          row = (int)r;
-          if (lane < TILE) req = s_treq[((i - 1) & 1) * TILE + lane];
-        }
-      }
-      need = req == ~0u ? 0 : 1 + (int)(req & 1u);
-      val = tbase[req == ~0u ? 0u : req >> 1];                         // every barrier: one load
+    // =============================== D: the scatter ============================================
+    for (;;) {
       arrive();
       hw_barrier();
-      // the next barrier (plain selects: a branchy update here left i and nq in scratch memory)
-      const int b0 = bk;
-      if (b0 == kBClaim) {
-        u = __builtin_amdgcn_readfirstlane(s_ctrl[0]);
-        if (u >= n_units) return false;
+      const uint32_t u = s_ctrl[0];
+      if (u >= n_units) break;
+      const int nq = a.n_ticks;
+      const int64_t env0 = (int64_t)u * TILE;
+      const int nE = (int)min((int64_t)TILE, n - env0);
+      arrive();
+      hw_barrier();
+#pragma unroll 1
+      for (int i = 0; i <= nq; ++i) {
+        if (i < nq && want_obs) {
+          const int e = lane % TILE;
+          const uint32_t ag = s_agent[(i & 1) * TILE + e];
+          if (e < nE && ((ag >> 24) & 1u))
+            scatter_env_part<WIN, P>(v, s_grid + (i & 1) * TILE * GS + e * GS,
+                                     s_inv + (i & 1) * TILE * kInvStride + e * kInvStride, ag,
+                                     s_obs + (i & 1) * obs_buf + e * F, lane / TILE);
+        }
+        arrive();
+        hw_barrier();
       }
-      nq = a.n_ticks;
-      nE = (int)min((int64_t)TILE, n - (int64_t)u * TILE);
-      i = b0 == kBC0 ? 0 : (b0 == kBTick ? i + 1 : i);
-      bk = b0 == kBClaim ? kBC0 : b0 == kBC0 ? kBTick : b0 == kBTick ? (i > nq ? kBEnd : kBTick) : kBClaim;
-      return true;
-    };
-    for (;;) {
-      if (!d_slot(va, ra, na)) break;
-      if (!d_slot(vb, rb, nb2)) break;
+      arrive();
+      hw_barrier();
     }
-    if (ra >= 0) decode(va, ra, na);                                   // the sets still in flight
-    if (rb >= 0) decode(vb, rb, nb2);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0 && s_ctrl[3]) latch_error(v.err, (int)s_ctrl[4], (int64_t)s_ctrl[3] - 1);
   } else if (wave < TW) {
     // =============================== E: the stores =============================================
     const int et = tid - 128;
@@ -801,6 +756,44 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     auto busy = [&]() __attribute__((always_inline)) -> bool {
       return jtail != jhead || __ballot(q.ph != kQIdle) != 0;
     };
+    // Policy actions: each walk fetches its items' table words with one LDS-DMA (global_load_lds,
+    // written by inline asm so that the compiler neither waits for it nor for the LDS it fills),
+    // a dummy one when the item asks for none, so that the fetch of the item kRtLag walks back is
+    // exactly the one vmcnt(kRtLag - 1) leaves waiting for (loads complete in order; any other
+    // VMEM op of this wave, a latched error, only makes the wait stricter).
+    const uint32_t* tbase = reinterpret_cast<const uint32_t*>(v.ttab ? (const void*)v.ttab : (const void*)v.task_tab);
+    auto fetch = [&](int q, uint32_t req) __attribute__((always_inline)) {
+      const uint32_t* gp = tbase + (req == ~0u ? 0u : req >> 1);
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(s_tval + q * 64));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // the slot's last reads are done
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(lds), "v"(gp));
+    };
+    // decode slot q's words (fetched kRtLag walks ago, or at the end: wait_all) into their label row
+    auto decode_slot = [&](int q, bool wait_all) __attribute__((always_inline)) {
+      const uint32_t prow = __builtin_amdgcn_readfirstlane(s_tpend[q]);
+      if (prow == ~0u) return;
+      if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRtLag - 1) : "memory");
+      uint32_t* R = s_rows + prow * RW;
+      const uint32_t req = lane < TILE ? s_treq[q * TILE + lane] : ~0u;
+      if (req != ~0u) {
+        const uint32_t word = s_tval[q * 64 + lane];
+        const uint32_t val = (req & 1u) ? word >> 16 : word & 0xffffu;
+        int err = 0, label = -2;
+        if (val & 0x8000u) label = go_leaf_action((val & 0x4000u) != 0, (int)((val >> 10) & 7u) - 1,
+                                                  (int)(val & 0x3ffu) - 1, err);
+        else err = CRAFT_EINVARIANT;                                   // (a reachable grid has its entry)
+        R[4 + lane] = (uint32_t)label;
+        if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + lane);
+      }
+      const uint32_t cnt = (uint32_t)__popcll(__ballot(req != ~0u));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        __hip_atomic_fetch_add(&R[0], 0u - cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        s_tpend[q] = ~0u;
+      }
+    };
     auto row_ctrl = [&](int row) __attribute__((always_inline)) -> uint32_t {
       return __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(&s_rows[row * RW], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -824,18 +817,14 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     // The teacher's schedule is a sequence of duties, each run once its condition holds; whenever
     // the next duty has to wait, the wave runs one BFS level (the single step() site: the BFS
     // state stays in registers instead of being spilled around several inlined copies).
-    enum { D_BAR, D_DECODE, D_DECODE_JOBS, D_WALK, D_WALK_JOBS, D_SYNC, D_DRAIN, D_EXIT };
+    enum { D_BAR, D_WALK, D_WALK_JOBS, D_SYNC, D_DRAIN, D_EXIT };
     enum { B_CLAIM, B_C0, B_TICK, B_END };
     int duty = D_BAR, bkind = B_CLAIM;
     int i = 0, nq = 0, nE = 0;
     uint32_t u = 0, gbase = 0;
-    // the walk's per-lane results between its two duties, and the table answer carried to the
-    // decode (the next interval with policy actions, the same one with label actions)
+    // the walk's per-lane results between its two duties
     int w_label = 0, w_need = 0;
-    uint32_t w_key = 0;                                                // as tt_key
-    uint32_t tt_val = 0, tt_key = 0;                                   // tt_key: p0 | dir<<8 | kind<<12 | conn<<20
-    bool tt_need = false;
-    int tt_row = 0, d_fall = 0;
+    uint32_t w_key = 0;                                                // p0 | dir<<8 | kind<<12 | conn<<20
     auto next_in_tick = [&]() __attribute__((always_inline)) -> int {   // after the barrier opening interval i
       return i < nq ? D_WALK : D_BAR;
     };
@@ -864,37 +853,6 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             gbase += nq;
             bkind = B_CLAIM;
           }
-          break;
-        }
-        case D_DECODE: {                                               // the table answers of the last walk
-          d_fall = 0;
-          const uint64_t bn = __ballot(tt_need);
-          if (tt_need) {
-            uint32_t* R = s_rows + tt_row * RW;
-            if (tt_val & 0x8000u) {
-              int err = 0;
-              R[4 + lane] = (uint32_t)go_leaf_action((tt_val & 0x4000u) != 0, (int)((tt_val >> 10) & 7u) - 1,
-                                                      (int)(tt_val & 0x3ffu) - 1, err);
-              if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + lane);
-            } else {
-              d_fall = 1;                                              // not computed: search the pristine row
-            }
-          }
-          const uint64_t bf = __ballot(d_fall != 0);
-          const uint32_t resolved = (uint32_t)__popcll(bn) - (uint32_t)__popcll(bf);
-          if (lane == 0 && resolved)
-            __hip_atomic_fetch_add(&s_rows[tt_row * RW], 0u - resolved, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-          tt_need = false;
-          duty = bf ? D_DECODE_JOBS : D_SYNC;
-          break;
-        }
-        case D_DECODE_JOBS: {
-          const uint64_t bf = __ballot(d_fall != 0);
-          if (jtail - jhead + (uint32_t)__popcll(bf) > (uint32_t)kRtQueue) { wait = true; break; }
-          push_jobs(bf, d_fall != 0, s_pristine + lane * GS, (tt_key >> 12) & 0xff, tt_key & 0xff,
-                    (tt_key >> 8) & 3, (tt_key >> 20) & 1, tt_row);
-          d_fall = 0;
-          duty = D_SYNC;
           break;
         }
         case D_WALK: {                                                 // item g = gbase + i, buffer i & 1
@@ -940,15 +898,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
 #if defined(RT_ABL) && (RT_ABL & 4)                                   // ablation: no BFS jobs
                 if (w_need == 2) { w_need = 0; w_label = CRAFT_STOP; }
 #endif
-                if (w_need == 1) {
-                  const uint32_t idx = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
-                  if (lsync) {
-                    tt_val = v.ttab[idx];                              // decoded in this interval
-                    tt_key = w_key;
-                  } else {
-                    req = idx;                                         // the scatter wave loads it
-                  }
-                }
+                if (w_need == 1) req = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
               }
             }
           }
@@ -958,13 +908,16 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             R[2] = u;
             R[3] = (uint32_t)((a.tick0 + i) % a.ring);
           }
-          if (!lsync) {
+          {
+            // decode the item fetched kRtLag walks ago (its slot; with label actions every item is
+            // decoded in its own interval), then fetch this one's
+            const int q = (int)(g & (kRtLag - 1));
+            if (!lsync) decode_slot(q, false);
             const bool any_req = __ballot(req != ~0u) != 0;          // (the whole wave votes)
-            if (lane < TILE) s_treq[p * TILE + lane] = req;
-            if (lane == 0) s_ctrl[5 + p] = any_req ? (uint32_t)row : ~0u;
+            if (lane < TILE) s_treq[q * TILE + lane] = req;
+            if (lane == 0) s_tpend[q] = any_req ? (uint32_t)row : ~0u;
+            fetch(q, req);
           }
-          tt_need = lsync && w_need == 1;
-          tt_row = row;
           duty = D_WALK_JOBS;
           break;
         }
@@ -979,7 +932,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           if (lane == 0)
             __hip_atomic_store(&s_rows[row * RW], kRowFill | pending, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-          duty = lsync ? D_DECODE : D_BAR;
+          duty = lsync ? D_SYNC : D_BAR;
+          if (lsync) decode_slot((int)((gbase + (uint32_t)i) & (kRtLag - 1)), true);   // (after the row's count)
           break;
         }
         case D_SYNC: {                                                 // label actions: item i complete
@@ -990,7 +944,9 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           duty = D_BAR;
           break;
         }
-        case D_DRAIN:                                                  // after the last barrier: the jobs left
+        case D_DRAIN:                                                  // after the last barrier: the fetches
+          if (!lsync)                                                  // and the BFS jobs left
+            for (int q = 0; q < kRtLag; ++q) decode_slot(q, true);
           if (busy()) wait = true;
           else duty = D_EXIT;
           break;
