@@ -92,7 +92,8 @@ enum {
 typedef struct craft_recipe {
   int32_t output;        /* kind id produced */
   int32_t workshop;      /* kind id of its `_at` workshop */
-  int32_t yield;         /* `_yield`, default 1 (craft.py:394) */
+  int32_t yield;         /* `_yield`, default 1, 1..255 (craft.py:394); a u8 count that would pass
+                            255 saturates and latches CRAFT_ERANGE */
   int32_t n_inputs;
   int32_t input_kind[CRAFT_MAX_INGREDIENTS];
   int32_t input_count[CRAFT_MAX_INGREDIENTS];

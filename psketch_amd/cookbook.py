@@ -75,6 +75,24 @@ class Cookbook:
             self.recipes[self.index.index(output)] = d
         self.n_kinds = len(self.index)
 
+    def primitives_for(self, goal):
+        """worlds/cookbook.py:28-52: the primitive kinds (and counts) that make `goal`, each
+        intermediate ingredient made ceil(count / _yield) times."""
+        out = {}
+        for ing, count in self.recipes[goal].items():
+            if not isinstance(ing, int):
+                continue                                     # _at, _yield
+            if ing in self.primitives:
+                parts, times = {ing: 1}, count
+            else:
+                parts = self.primitives_for(ing)
+                times = -(-count // self.recipes[ing].get("_yield", 1))
+            for k, v in parts.items():
+                if k not in self.primitives:
+                    raise AssertionError(f"kind {k} is not a primitive")
+                out[k] = out.get(k, 0) + v * times
+        return out
+
 
 _FEXP = re.compile(r"(.*)\[(.*)\]")
 

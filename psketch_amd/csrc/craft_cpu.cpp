@@ -177,8 +177,8 @@ int satisfies(const craft_sim* s, const uint8_t* g, const uint8_t* iv, const Age
 }
 
 // CraftState.step (craft.py:332-424) on grid g and inventory iv; m: the cleared-cell mask.
-void transition(const craft_sim* s, uint8_t* g, uint8_t* iv, Agent& a, uint32_t* m, int act, bool& inv_changed,
-                bool& mask_changed) {
+void transition(craft_sim* s, uint8_t* g, uint8_t* iv, Agent& a, uint32_t* m, int act, bool& inv_changed,
+                bool& mask_changed, int64_t slot) {
   const int H = s->H;
   int dx = 0, dy = 0, ndir = a.dir;
   if (act < CRAFT_USE) {                             // moves always turn (craft.py:341-352)
@@ -195,7 +195,8 @@ void transition(const craft_sim* s, uint8_t* g, uint8_t* iv, Agent& a, uint32_t*
       if (thing != 0) {
         const int cls = s->cfg.kind_class[thing];
         if (cls == CRAFT_KIND_GRABBABLE) {           // craft.py:383-386
-          iv[thing] = (uint8_t)(iv[thing] + 1);
+          if (iv[thing] == 255) latch(s, CRAFT_ERANGE, slot);   // u8 count would wrap
+          else iv[thing] = (uint8_t)(iv[thing] + 1);
           g[c] = 0;
           m[c >> 5] |= 1u << (c & 31);
           inv_changed = mask_changed = true;
@@ -206,7 +207,9 @@ void transition(const craft_sim* s, uint8_t* g, uint8_t* iv, Agent& a, uint32_t*
             bool have = true;
             for (int q = 0; q < rc.n_inputs; ++q) have = have && iv[rc.input_kind[q]] >= rc.input_count[q];
             if (!have) continue;
-            iv[rc.output] = (uint8_t)(iv[rc.output] + 1);     // `_yield` 1 (validated at create)
+            const int made = iv[rc.output] + rc.yield;      // `_yield` (craft.py:394), 1..255
+            if (made > 255) latch(s, CRAFT_ERANGE, slot);   // u8 count would wrap: saturate
+            iv[rc.output] = (uint8_t)std::min(made, 255);
             for (int q = 0; q < rc.n_inputs; ++q) iv[rc.input_kind[q]] = (uint8_t)(iv[rc.input_kind[q]] - rc.input_count[q]);
             inv_changed = true;
           }
@@ -505,7 +508,7 @@ void tick_slot(craft_sim* s, int64_t i, const TickIn& in, TickAcc& acc, uint8_t*
       } else {
         const int ox = a.x, oy = a.y;
         bool ic = false, mc = false;
-        transition(s, g, iv, a, m, act, ic, mc);
+        transition(s, g, iv, a, m, act, ic, mc, slot);
         code = transition_code(ox, oy, a, ic);
       }
     }
@@ -1034,7 +1037,7 @@ int craft_transition(craft_sim_t* s, const int32_t* src, const int32_t* dst, con
           } else if (act >= 0) {
             const int ox = a.x, oy = a.y;
             bool ic = false, mc = false;
-            transition(s, g.data(), iv, a, m, act, ic, mc);
+            transition(s, g.data(), iv, a, m, act, ic, mc, slot);
             code = transition_code(ox, oy, a, ic);
           }
           s->state[dslot] = pack_state(a);

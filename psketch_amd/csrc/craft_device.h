@@ -63,7 +63,7 @@ struct SimView {
   uint64_t tt_slot[2];
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |
-  // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16.  Kernels copy the table to LDS.
+  // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16 | yield<<24.  Kernels copy the table to LDS.
   // (As kernel-argument words they cost ~50 scalar registers, which spilled.)
   const uint32_t* rcw;
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
@@ -294,7 +294,7 @@ __device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, b
 template <bool RCV = false>
 __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
-                                           bool& mask_changed, uint32_t rcv = 0u) {
+                                           bool& mask_changed, uint32_t rcv = 0u, int64_t slot = -1) {
   auto rword = [&](int w) -> uint32_t {
     if constexpr (RCV) return __builtin_amdgcn_readlane(rcv, w);
     else return __builtin_amdgcn_readfirstlane(rc[w]);
@@ -315,7 +315,8 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
       if (thing != 0) {
         const int cls = kind_class(v, thing);
         if (cls == CRAFT_KIND_GRABBABLE) {           // craft.py:383-386
-          iv[thing] = (uint8_t)(iv[thing] + 1);
+          if (iv[thing] == 255) latch_error(v.err, CRAFT_ERANGE, slot);   // u8 count would wrap
+          else iv[thing] = (uint8_t)(iv[thing] + 1);
           g[c] = 0;
           mask_set(m, c);
           inv_changed = mask_changed = true;
@@ -338,7 +339,9 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
                               (n_in < 3 || h2 >= c2) && (n_in < 4 || h3 >= c3);
             if (!have) continue;
             const int out = a0 & 0xff;
-            iv[out] = (uint8_t)(iv[out] + 1);        // `_yield` 1 (validated at create)
+            const int made = iv[out] + (int)(a2 >> 24);      // `_yield` (craft.py:394), 1..255
+            if (made > 255) latch_error(v.err, CRAFT_ERANGE, slot);   // u8 count would wrap: saturate
+            iv[out] = (uint8_t)(made > 255 ? 255 : made);
             if (n_in > 0) iv[k0] = (uint8_t)(iv[k0] - c0);
             if (n_in > 1) iv[k1] = (uint8_t)(iv[k1] - c1);
             if (n_in > 2) iv[k2] = (uint8_t)(iv[k2] - c2);

@@ -37,7 +37,7 @@ inline int validate_config(const craft_config_t* c, std::string& msg) {
     const craft_recipe_t& rc = c->recipe[r];
     if (rc.output <= 0 || rc.output >= c->n_kinds || rc.workshop <= 0 || rc.workshop >= c->n_kinds ||
         rc.n_inputs < 1 || rc.n_inputs > CRAFT_MAX_INGREDIENTS) { msg = "bad recipe"; return CRAFT_EINVAL; }
-    if (rc.yield != 1) { msg = "_yield != 1 is not supported (u8 inventory counts)"; return CRAFT_EINVAL; }
+    if (rc.yield < 1 || rc.yield > 255) { msg = "recipe _yield outside 1..255"; return CRAFT_EINVAL; }
     for (int i = 0; i < rc.n_inputs; ++i)
       if (rc.input_kind[i] <= 0 || rc.input_kind[i] >= c->n_kinds || rc.input_count[i] < 1 ||
           rc.input_count[i] > 255) { msg = "bad recipe input"; return CRAFT_EINVAL; }

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(NT, WPE) void rollout_kernel(SimView v, RolloutArgs
         const int fc = (s.x + dir_dx(s.dir)) * v.H + (s.y + dir_dy(s.dir));   // what USE clears
 #ifndef CRAFT_ABL_NOTRANS
         if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-        else transition<true>(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed, rcv);
+        else transition<true>(v, s_rc, g, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot);
 #endif
         if (mask_changed) {
           const uint32_t nc = (clr >> 24) & 3;

@@ -405,7 +405,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           const int fc = (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir));   // what USE clears
           if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-          else transition<true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv);
+          else transition<true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot);
           if (mask_changed) {
             ++ncl;
             chg = 1u + (uint32_t)fc;

@@ -383,6 +383,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
       b[3 + 2 * i] = (uint8_t)rc.input_kind[i];
       b[4 + 2 * i] = (uint8_t)rc.input_count[i];
     }
+    b[11] = (uint8_t)rc.yield;                       // 1..255 (validated)
     for (int q = 0; q < 3; ++q)
       rcw[3 * r + q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) | ((uint32_t)b[4 * q + 2] << 16) |
                        ((uint32_t)b[4 * q + 3] << 24);

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
           latch_error(v.err, CRAFT_EBADACTION, slot);
         } else {
           const int ox = s.x, oy = s.y;
-          transition<true>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw);
+          transition<true>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw, slot);
           code = transition_code(ox, oy, s, inv_changed);
         }
       }

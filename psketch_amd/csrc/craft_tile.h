@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
             latch_error(v.err, CRAFT_EBADACTION, slot);
           } else {
             const int ox = s.x, oy = s.y;
-            transition<TILE == 64>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw[0]);
+            transition<TILE == 64>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw[0], slot);
             code = transition_code(ox, oy, s, inv_changed);
           }
         }
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
           latch_error(v.err, CRAFT_EBADACTION, slot);
         } else if (act >= 0) {
           const int ox = s.x, oy = s.y;
-          transition<TILE == 64>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw[0]);
+          transition<TILE == 64>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw[0], slot);
           code = transition_code(ox, oy, s, inv_changed);
         }
         if (dslot != slot) inv_changed = mask_changed = true;   // copy-on-step
