@@ -40,6 +40,10 @@ struct SimView {
   uint4* mask;
   const uint16_t* task_tab;   // [n_tasks]: goal | arg_kind<<4 | n_subtasks<<12
   const int32_t* task_sub;    // [n_tasks][4] subtask ids
+  // the hint walk tabulated (craft_host.h hint_tables): [CRAFT_MAX_TASKS][4] descriptor words,
+  // then hint_bytes leaf bytes
+  const uint32_t* hint;
+  int32_t hint_bytes;
   int64_t* stats_part;        // [n_tiles][4]
   int32_t* err;               // [4] {code, pad, slot lo, slot hi}
   int64_t n_envs, env_base;

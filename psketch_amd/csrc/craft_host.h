@@ -87,6 +87,89 @@ inline void task_tables(const craft_config_t& cfg, uint16_t* tab, int32_t* sub) 
   }
 }
 
+// ---- the hint walk, tabulated (craft_rollout_teach's teacher wave) ---------------------------
+// hint_leaf (craft_teach.h: find_incomplete_subtask, teachers/base.py:10-25, and the leaf's
+// action, demonstration.py:12-30) reads satisfies() (craft.py:285-294) of nodes reachable from the
+// task, and each node's is one predicate: get/make X -> inventory[X] > 0, go X -> the facing cell
+// is X, any other goal -> never satisfied.  For a task with at most kHintPreds distinct predicates
+// the leaf is a function of their truth values alone; hint_tables evaluates hint_leaf's walk for
+// every combination.  desc[4t], desc[4t+1]: predicate j in byte j (bit 7 used, bit 6 a facing
+// test, else an inventory test, bits 0-5 the kind); desc[4t+2]: the byte offset of the task's
+// 2^P leaves, or kHintWalk (more predicates, or past kHintLeafCap bytes: the kernel walks).
+// Leaf byte: a go[] kind, kHintStop, kHintUse or kHintErr (the reference raises).
+constexpr int kHintPreds = 8, kHintLeafCap = 2048;
+constexpr uint8_t kHintErr = 0xff, kHintStop = 0xfe, kHintUse = 0xfd;
+constexpr uint32_t kHintWalk = 1u << 31;
+inline void hint_tables(const craft_config_t& cfg, const uint16_t* tab, const int32_t* sub, uint32_t* desc,
+                        std::vector<uint8_t>& leaf) {
+  leaf.clear();
+  auto key = [&](int t) -> int {                 // the node's predicate: kind | 0x40 facing; -1 none
+    const int goal = tab[t] & 0xf, arg = (tab[t] >> 4) & 0xff;
+    if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) return arg & 0x3f;
+    if (goal == CRAFT_GOAL_GO) return 0x40 | (arg & 0x3f);
+    return -1;
+  };
+  for (int t = 0; t < CRAFT_MAX_TASKS; ++t) {
+    desc[4 * t] = desc[4 * t + 1] = desc[4 * t + 3] = 0;
+    desc[4 * t + 2] = kHintWalk;
+    if (t >= cfg.n_tasks) continue;
+    int keys[CRAFT_MAX_TASKS], nk = 0;
+    bool seen[CRAFT_MAX_TASKS] = {};
+    int stack[CRAFT_MAX_TASKS], top = 0;
+    stack[top++] = t;
+    seen[t] = true;
+    while (top) {                                // every node reachable from t
+      const int node = stack[--top];
+      const int k = key(node);
+      bool have = k < 0;
+      for (int i = 0; i < nk && !have; ++i) have = keys[i] == k;
+      if (!have) keys[nk++] = k;
+      const int ns = (tab[node] >> 12) & 0xf;
+      for (int q = 0; q < ns && q < CRAFT_MAX_SUBTASKS; ++q) {
+        const int c = sub[CRAFT_MAX_SUBTASKS * node + q];
+        if (c >= 0 && c < CRAFT_MAX_TASKS && !seen[c]) { seen[c] = true; stack[top++] = c; }
+      }
+    }
+    if (nk > kHintPreds || leaf.size() + ((size_t)1 << nk) > (size_t)kHintLeafCap) continue;
+    for (int j = 0; j < nk; ++j) desc[4 * t + (j >> 2)] |= (0x80u | (uint32_t)keys[j]) << (8 * (j & 3));
+    desc[4 * t + 2] = (uint32_t)leaf.size();
+    for (uint32_t bits = 0; bits < (1u << nk); ++bits) {
+      auto sat = [&](int node) -> int {
+        const int k = key(node);
+        if (k < 0) return -1;
+        for (int j = 0; j < nk; ++j)
+          if (keys[j] == k) return (int)((bits >> j) & 1u);
+        return -1;
+      };
+      // hint_leaf's walk, statement for statement
+      uint8_t out;
+      if (sat(t) == 1) {
+        out = kHintStop;
+      } else {
+        int node = t;
+        bool raised = false;
+        for (int guard = 0; guard < CRAFT_MAX_TASKS; ++guard) {
+          const int ns = (tab[node] >> 12) & 0xf;
+          if (ns == 0) break;
+          const int32_t* sb = sub + CRAFT_MAX_SUBTASKS * node;
+          int chosen = sb[ns - 1];
+          bool last = true;
+          for (int q = 0; q + 1 < ns; ++q)
+            if (sat(sb[q]) != 1) { chosen = sb[q]; last = false; break; }
+          if (last && sat(chosen) == 1) { raised = true; break; }
+          node = chosen;
+        }
+        const int goal = tab[node] & 0xf;
+        out = raised ? kHintErr
+            : goal == CRAFT_GOAL_USE ? kHintUse
+            : goal == CRAFT_GOAL_GO ? (uint8_t)((tab[node] >> 4) & 0xff)
+            : kHintErr;
+      }
+      leaf.push_back(out);
+    }
+  }
+}
+
 // craft_pool_load's checks of one scenario grid g (W*H kind ids, x-major), pool row `index`:
 // kind ids in range, and a border ring of inert, non-target kinds (make_data.py:108-112 fills
 // it with `boundary`; the kernels never index past it, and the teacher's band-layout BFS leaves

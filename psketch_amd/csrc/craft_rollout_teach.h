@@ -11,24 +11,27 @@
 //   wave 0       C(i+1): the transitions (one lane per env) into grid / inventory buffer (i+1) & 1;
 //   wave 1       D(i):   the observation scatter of item i from buffer i & 1;
 //   waves 2..6   E(i-1): the observation stream of the item before, to HBM; wave 2 also stores the
-//                        teacher's finished label rows, in item order;
+//                        teacher's finished label rows, in item order, waves 3..6 item i's done,
+//                        success, reward and action record (one array each);
 //   wave 7       T(i):   the teacher on item i's post-step rows (buffer i & 1, which C(i+2)
 //                        overwrites one interval later).
 //
 // The teacher wave.  Its walk (find_incomplete_subtask, one lane per env) must finish inside the
 // interval, but a BFS chain (~30 dependent levels) is longer than an interval (~4 us), so the
 // BFS is decoupled from the item:
-//   * a go[X] leaf on a pristine grid (no cell cleared this episode) issues the teacher table's
-//     answer load (craft_teach.h teach table) and decodes it one interval later (policy actions)
-//     or right away (label actions);
+//   * the hint walk (find_incomplete_subtask) is a table lookup: the leaf as a function of the
+//     task's satisfies() predicates (craft_host.h hint_tables), three rounds of LDS loads;
+//   * a go[X] leaf on a grid the teacher table lists (the pool row minus a subset of its listed
+//     clearable cells) issues the table's answer load (LDS-DMA) and decodes it kRtLag walks later
+//     (policy actions) or right away (label actions);
 //   * any other go[X] leaf becomes a BFS job: the leaf lane builds the band bitsets of its grid
 //     row while the row is still current and queues them in LDS;
 //   * between its own duties the wave runs the queued jobs, one BFS level per step on 16 quads
 //     (lane q of a quad: the states entered by action q, as bfs_closest<NW, 4>), each quad a
 //     small state machine (forward, reachability flood, backward), taking a new job as soon as
-//     its last one ends.  Before every barrier it steps until all other waves have arrived (an
-//     LDS arrival counter), so the BFS fills the interval's slack and never holds the barrier
-//     for more than one level.
+//     its last one ends.  Before every barrier, with jobs queued, it steps until all other waves
+//     have arrived (an LDS arrival counter), so the BFS fills the interval's slack and never
+//     holds the barrier for more than one level; with none it goes straight to the barrier.
 // Labels go into LDS label rows (item g -> row g & 7, with a count of labels still pending); the
 // teacher wave issues no global store at all (a store would make its next table load wait:
 // vmcnt counts loads and stores in issue order).  Wave 2 stores each row once complete, strictly
@@ -43,17 +46,26 @@
 // Results are identical to n_ticks craft_step_teach calls with the same action sources (tests:
 // tests/test_gpu_rollout_teach.py, tick by tick at 65,536 envs and against the oracle).
 #pragma once
+#include "craft_host.h"
 #include "craft_obs.h"
 #include "craft_teach.h"
 
 namespace craft {
 
 constexpr int kRtThreads = 512;        // C, D, 5 streaming waves, the teacher
-constexpr int kRtRows = 8;             // label rows in flight: item g -> row g & 7
+#ifndef RT_ROWS
+#define RT_ROWS 8
+#endif
+#ifndef RT_LAG
+#define RT_LAG 4
+#endif
+constexpr int kRtRows = RT_ROWS;       // label rows in flight: item g -> row g & (kRtRows - 1)
 constexpr int kRtQueue = 32;           // BFS jobs waiting for a quad
 // Table answers are fetched kRtLag walks ahead of their decode: a load from the table (hundreds of
 // MB, random rows) takes longer than an interval while the store stream saturates HBM.
-constexpr int kRtLag = 4;
+constexpr int kRtLag = RT_LAG;
+static_assert(kRtRows <= 16 && (kRtRows & (kRtRows - 1)) == 0 && (kRtLag & (kRtLag - 1)) == 0 && kRtLag < kRtRows,
+              "rows and lag: powers of two, a fetched item's row still held when it is decoded");
 // label row control word: 0 free; kRowFill | pending labels while the teacher fills it (== kRowFill:
 // complete); kRowStoring while wave 2 copies it out
 constexpr uint32_t kRowFill = 1u << 30, kRowStoring = 1u << 29;
@@ -62,12 +74,13 @@ constexpr uint32_t kRowFill = 1u << 30, kRowStoring = 1u << 29;
 constexpr uint32_t kRtSpinCap = 1u << 22;
 
 // LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation rows [2][up16(TILE*F)] |
-// inventory rows [2][TILE][36] | agent words [2][TILE] | teacher info words [2][TILE] | task table
+// inventory rows [2][TILE][36] | agent words [2][TILE] | teacher info words [2][TILE] | the tick's
+// outputs [2][TILE][2] | task table
 // [64] u16 | subtasks [64][4] | recipe words [16][3] | control words [8] | label rows
 // [8][4 + TILE] | BFS job queue [32][2 NW + 1] | table requests [4][TILE] | table words [4][64] |
-// their rows [4] | clearable cells [TILE][2]
+// their rows [4] | clearable cells [TILE][2] | hint table: descriptors [64][4], leaf bytes [2048]
 struct RtLds {
-  int pristine, obs, inv, agent, tinfo, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, bytes;
+  int pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint, bytes;
 };
 __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -77,7 +90,8 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.inv = l.obs + 2 * up16(tile * F);
   l.agent = up16(l.inv + 2 * tile * kInvStride);
   l.tinfo = l.agent + 2 * tile * 4;
-  l.task = l.tinfo + 2 * tile * 4;
+  l.cout = l.tinfo + 2 * tile * 4;                         // [2][TILE][2] C's outputs: flags, action
+  l.task = l.cout + 2 * tile * 8;
   l.tsub = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.rc = l.tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4;
   l.ctrl = l.rc + CRAFT_MAX_RECIPES * 12;
@@ -87,7 +101,8 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.tval = l.treq + kRtLag * tile * 4;                     // [kRtLag][64] the words fetched (LDS-DMA)
   l.tpend = l.tval + kRtLag * 64 * 4;                      // [kRtLag] their label rows (~0: none)
   l.tcell = l.tpend + kRtLag * 4;                          // [tile][2] each env's listed clearable cells
-  l.bytes = up16(l.tcell + tile * 8);
+  l.hint = up16(l.tcell + tile * 8);                       // craft_host.h hint_tables
+  l.bytes = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;
   return l;
 }
 // envs per tile: 32 for 3x3 windows (as the split rollout kernel), 16 for wider ones (their
@@ -117,11 +132,11 @@ __device__ __forceinline__ int64_t rt_where(uint32_t wait, uint32_t item, uint32
   return (int64_t)(((uint64_t)wait << 60) | ((uint64_t)(item & 0xfffffffu) << 32) | state);
 }
 
-// Job meta word: band start cell p0 (bits 0-7), dir (8-9), connected (10), label row (11-13),
-// env in the tile (14-19).
+// Job meta word: band start cell p0 (bits 0-7), dir (8-9), connected (10), label row (11-14),
+// env in the tile (15-20).
 __device__ __forceinline__ uint32_t rt_job_meta(int p0, int d0, int conn, int row, int env) {
   return (uint32_t)p0 | ((uint32_t)d0 << 8) | ((uint32_t)conn << 10) | ((uint32_t)row << 11) |
-         ((uint32_t)env << 14);
+         ((uint32_t)env << 15);
 }
 
 template <int WIN, int TILE, int NW>
@@ -146,6 +161,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   // [2][TILE] x | y<<8 | dir<<16 | live<<24 | frozen<<25 | cells cleared this episode (63 = more) << 26
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
   uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.tinfo);  // [2][TILE] task|conn<<8|scen<<10
+  // [2][TILE] done | (succ + 1) << 1 | counted << 3, and the recorded action: stored by waves 3-6
+  uint2* s_cout = reinterpret_cast<uint2*>(smem + lay.cout);
   uint32_t* s_treq = reinterpret_cast<uint32_t*>(smem + lay.treq);    // [kRtLag][TILE] ttab index, ~0 = none
   uint32_t* s_tval = reinterpret_cast<uint32_t*>(smem + lay.tval);    // [kRtLag][64] fetched table words
   uint32_t* s_tpend = reinterpret_cast<uint32_t*>(smem + lay.tpend);  // [kRtLag] their label rows, ~0 none
@@ -153,14 +170,35 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
+  const uint4* s_hdesc = reinterpret_cast<const uint4*>(smem + lay.hint);   // [task]: predicates, leaf offset
+  const uint8_t* s_hleaf = smem + lay.hint + CRAFT_MAX_TASKS * 16;
   // [0] the claimed unit, [1] barrier arrivals, [2] items whose labels are complete (label actions),
-  // [3], [4] unused
+  // [3] barriers the teacher has arrived at, [4] unused
   uint32_t* s_ctrl = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
   uint32_t* s_rows = reinterpret_cast<uint32_t*>(smem + lay.rows);    // [8][RW]: ctrl, tag = g + 1, tile, ring slot, labels
   uint32_t* s_jobs = reinterpret_cast<uint32_t*>(smem + lay.jobs);    // [32][JW]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t n = v.n_envs;
+#ifdef CRAFT_STAMPS
+  // diagnostic builds (tools/rt_stamps.py): per wave 8 shader-clock sums, v.stamps[wg][wave][8]:
+  // [0] the hardware barrier, [1] wave 2's wait for the teacher, [2] the role's work (C tick,
+  // D scatter, E stream; T walk), T: [3] decode, [4] jobs, [5] BFS steps, [6] idle, [7] steps;
+  // wave 0 [6] the workgroup's s_memrealtime span, [7] its shader-clock span
+  // (sums in LDS past the carve, so that the stamps cost the waves no registers)
+  unsigned long long* stt = reinterpret_cast<unsigned long long*>(smem + lay.bytes) + wave * 8;
+  if (lane < 8) stt[lane] = 0ull;
+  const uint64_t st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = __builtin_amdgcn_s_memrealtime();
+#define RT_CLK() __builtin_amdgcn_s_memtime()
+#define RT_ACC(k, t0)                                                                              \
+  do {                                                                                             \
+    const unsigned long long dt_ = __builtin_amdgcn_s_memtime() - (t0);                            \
+    if (lane == 0) __hip_atomic_fetch_add(&stt[k], dt_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); \
+  } while (0)
+#else
+#define RT_CLK() 0ull
+#define RT_ACC(k, t0) ((void)(t0))
+#endif
   const bool want_obs = a.obs != nullptr;
   const bool lsync = a.lsync != 0;                                    // labels feed some env's actions
   const int n_tiles = (int)((n + TILE - 1) / TILE);
@@ -171,6 +209,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   for (int t = tid; t < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS; t += NT)
     s_tsub[t] = t < v.n_tasks * CRAFT_MAX_SUBTASKS ? v.task_sub[t] : 0;
   for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += NT) s_rc[t] = v.rcw[t];
+  for (int t = tid; t < CRAFT_MAX_TASKS * 4 + ((v.hint_bytes + 3) >> 2); t += NT)
+    reinterpret_cast<uint32_t*>(smem + lay.hint)[t] = v.hint[t];
   {
     uint4* z = reinterpret_cast<uint4*>(s_obs);
     for (int i = tid; i < (2 * obs_buf >> 4); i += NT) z[i] = make_uint4(0, 0, 0, 0);
@@ -181,8 +221,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   __syncthreads();                                                    // (not counted: nb starts at 0)
 
   // Barriers.  Every wave adds one arrival per barrier before s_barrier; the teacher wave first
-  // runs BFS steps until every other wave has arrived; wave 2 stores label rows until the teacher
-  // has.  (A plain s_barrier behind the wave's own LDS accesses: nothing else is handed over.)
+  // runs its queued BFS steps until every other wave has arrived; wave 2 stores label rows until
+  // the teacher has (s_ctrl[3]).  (A plain s_barrier behind the wave's own LDS accesses: nothing else is handed over.)
   uint32_t nb = 0;                                                    // barriers passed
   auto arrive = [&]() __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -194,8 +234,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   };
   auto hw_barrier = [&]() __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t tb = RT_CLK();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    RT_ACC(0, tb);
     ++nb;
   };
 
@@ -322,7 +364,6 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     // ---- C: tick k (item g) into buffer k & 1 (trainers/imitation.py:43-73) ----
     auto tick_c = [&](int k, uint32_t g) __attribute__((always_inline)) {
       const int64_t tick = a.tick0 + k;
-      const int64_t r = tick % a.ring;
       int d = 0, succ = -1, counted = 0, act = 0;
       uint8_t* gr = grid_of(k);
       uint8_t* iv = inv_of(k);
@@ -337,6 +378,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       }
       s = unpack_state(st);
+      const uint64_t tc0 = RT_CLK();
       if (live) {
         if (sync == 1) {                                               // bring the buffer up to date
           const uint32_t* src = reinterpret_cast<const uint32_t*>(grid_of(k + 1));
@@ -363,6 +405,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         }
         sync = sync ? 2 : 1;
         chg = 0;
+        RT_ACC(4, tc0);
+        const uint64_t tc1 = RT_CLK();
         if (a.actions) {
           act = a.actions[(int64_t)k * n + slot];
         } else {
@@ -400,6 +444,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           s.frozen = 1;
           s.timer = max(s.timer, 0);
         }
+        RT_ACC(5, tc1);
+        const uint64_t tc2 = RT_CLK();
         if (!d) {
           bool inv_changed = false, mask_changed = false;
           uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -415,11 +461,14 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           }
         }
         st = pack_state(s);
-        const int64_t o = r * n + slot;
-        if (a.done) a.done[o] = (uint8_t)d;
-        if (a.sat) a.sat[o] = (int8_t)succ;
-        if (a.reward) a.reward[o] = (counted && d && succ == 1) ? 1.0f : 0.0f;
-        if (a.rec) a.rec[o] = counted ? act : -1;                     // action_seqs, imitation.py:59-61
+        RT_ACC(3, tc2);
+        const uint64_t tc3 = RT_CLK();
+        // done, success, reward and the recorded action (action_seqs, imitation.py:59-61) leave
+        // from the streaming waves, one array each
+        s_cout[(k & 1) * TILE + lane] = make_uint2((uint32_t)d | ((uint32_t)(succ + 1) << 1) | ((uint32_t)counted << 3) |
+                                                       (1u << 4),                          // (stored)
+                                                   (uint32_t)(counted ? act : -1));
+        RT_ACC(1, tc3);
       }
       const uint64_t bs = __ballot(live && counted && d && succ == 1);
       const uint64_t be = __ballot(live && counted && d);
@@ -428,6 +477,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       n_end += (uint32_t)__popcll(be);
       n_step += (uint32_t)__popcll(bt);
       if (lane < TILE) {
+        if (!live) s_cout[(k & 1) * TILE + lane] = make_uint2(0u, 0u);
         s_agent[(k & 1) * TILE + lane] =
             live ? ((uint32_t)s.x | ((uint32_t)s.y << 8) | ((uint32_t)s.dir << 16) | (1u << 24) |
                     ((uint32_t)s.frozen << 25) | ((uint32_t)min(ncl, 63) << 26))
@@ -470,7 +520,9 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       arrive();
       hw_barrier();                                                   // C(0) done
       for (int i = 0; i <= nq; ++i) {
+        const uint64_t tc = RT_CLK();
         if (lane < TILE && i + 1 < nq) tick_c(i + 1, gbase + i + 1);
+        RT_ACC(2, tc);
         arrive();
         hw_barrier();
       }
@@ -493,6 +545,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       hw_barrier();
 #pragma unroll 1
       for (int i = 0; i <= nq; ++i) {
+        const uint64_t td = RT_CLK();
         if (i < nq && want_obs) {
           const int e = lane % TILE;
           const uint32_t ag = s_agent[(i & 1) * TILE + e];
@@ -501,6 +554,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
                                      s_inv + (i & 1) * TILE * kInvStride + e * kInvStride, ag,
                                      s_obs + (i & 1) * obs_buf + e * F, lane / TILE);
         }
+        RT_ACC(2, td);
         arrive();
         hw_barrier();
       }
@@ -543,9 +597,11 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     };
     auto e_barrier = [&]() __attribute__((always_inline)) {
       arrive();
+      const uint64_t tw = RT_CLK();
       if (wave == 2) {
         // keep storing until the teacher has arrived too (it may wait for a free row)
-        for (uint32_t spins = 0; arrivals() < (uint32_t)NWAVE * (nb + 1); ++spins) {
+        for (uint32_t spins = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                     &s_ctrl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < nb + 1; ++spins) {
           store_rows(1);
           __builtin_amdgcn_s_sleep(1);
           if (spins > kRtSpinCap) {                                    // never hang
@@ -554,6 +610,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           }
         }
       }
+      RT_ACC(1, tw);
       hw_barrier();
     };
     uint32_t gbase = 0;
@@ -567,6 +624,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       const int nE = (int)min((int64_t)TILE, n - env0);
       e_barrier();
       for (int i = 0; i <= nq; ++i) {
+        const uint64_t te = RT_CLK();
         if (i >= 1 && want_obs) {
           const int64_t r = (a.tick0 + i - 1) % a.ring;
           void* out = static_cast<uint8_t*>(a.obs) + r * n * (int64_t)F * (v.obs_fmt == CRAFT_OBS_F32 ? 4 : v.obs_fmt == CRAFT_OBS_BF16 ? 2 : 1);
@@ -578,6 +636,18 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           }
         }
         if (wave == 2) store_rows(2);
+        if (i < nq && wave >= 3 && lane < nE) {                       // tick i's outputs: one array per wave
+          const uint2 c = s_cout[(i & 1) * TILE + lane];
+          const int64_t o = ((a.tick0 + i) % a.ring) * n + env0 + lane;
+          const int d = (int)(c.x & 1u), succ = (int)((c.x >> 1) & 3u) - 1, counted = (int)((c.x >> 3) & 1u);
+          if (c.x & (1u << 4)) {
+            if (wave == 3 && a.done) a.done[o] = (uint8_t)d;
+            if (wave == 4 && a.sat) a.sat[o] = (int8_t)succ;
+            if (wave == 5 && a.reward) a.reward[o] = (counted && d && succ == 1) ? 1.0f : 0.0f;
+            if (wave == 6 && a.rec) a.rec[o] = (int32_t)c.y;
+          }
+        }
+        RT_ACC(2, te);
         e_barrier();
       }
       e_barrier();
@@ -603,7 +673,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     auto finish = [&](int label, int err) __attribute__((always_inline)) {
       // lane 0 of the quad: the label into its row, one pending label fewer
       if (ql == 0) {
-        const int row = (q.meta >> 11) & 7, env = (q.meta >> 14) & 63;
+        const int row = (q.meta >> 11) & (kRtRows - 1), env = (q.meta >> 15) & 63;
         uint32_t* R = s_rows + row * RW;
         R[4 + env] = (uint32_t)label;
         if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + env);
@@ -771,10 +841,15 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     };
     // decode slot q's words (fetched kRtLag walks ago, or at the end: wait_all) into their label row
     auto decode_slot = [&](int q, bool wait_all) __attribute__((always_inline)) {
+      const uint64_t tq = RT_CLK();
       const uint32_t prow = __builtin_amdgcn_readfirstlane(s_tpend[q]);
-      if (prow == ~0u) return;
+      if (prow == ~0u) { RT_ACC(3, tq); return; }
+#if defined(RT_ABL) && (RT_ABL & 8)                                   // ablation (timing only): no wait
+      if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
       if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRtLag - 1) : "memory");
+#endif
       uint32_t* R = s_rows + prow * RW;
       const uint32_t req = lane < TILE ? s_treq[q * TILE + lane] : ~0u;
       if (req != ~0u) {
@@ -793,6 +868,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         __hip_atomic_fetch_add(&R[0], 0u - cnt, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         s_tpend[q] = ~0u;
       }
+      RT_ACC(3, tq);
     };
     auto row_ctrl = [&](int row) __attribute__((always_inline)) -> uint32_t {
       return __builtin_amdgcn_readfirstlane(
@@ -831,9 +907,14 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     uint32_t steps_run = 0;                                            // BFS levels this launch
     for (uint32_t idle_spins = 0;;) {
       bool wait = false;
+      const uint64_t tt = RT_CLK();
+      const int duty0 = duty;
       switch (duty) {
         case D_BAR: {
-          if (arrivals() < (uint32_t)NWAVE * nb + (NWAVE - 1)) { wait = true; break; }
+          // with BFS work queued, run it until every other wave has arrived; without, go straight
+          // to the barrier
+          if (busy() && arrivals() < (uint32_t)NWAVE * nb + (NWAVE - 1)) { wait = true; break; }
+          if (lane == 0) __hip_atomic_store(&s_ctrl[3], nb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           arrive();
           hw_barrier();
           if (bkind == B_CLAIM) {
@@ -865,31 +946,60 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           w_need = 0;                                                  // 1: a table answer, 2: a BFS job
           uint32_t req = ~0u;                                          // (policy actions) the ttab index asked
           if (lane < nE) {
+            // the walk's loads in three rounds, each issued together: the agent and task words and
+            // the row's listed clearable cells; the facing cell, the hint descriptor, the inventory
+            // and the listed cells' kinds now; the hint leaf
             const uint32_t ag = s_agent[p * TILE + lane];
             const uint32_t ti = s_tinfo[p * TILE + lane];
-            if (((ag >> 24) & 1u) && ((ag >> 25) & 1u)) {
+            const uint32_t cw0 = s_tcell[2 * lane], cw1 = s_tcell[2 * lane + 1];
+            const bool live_env = (ag >> 24) & 1u;
+            const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
+            const uint8_t* gr = s_grid + p * TILE * GS + lane * GS;
+            const int facing = gr[live_env ? (x + dir_dx(dir)) * H + (y + dir_dy(dir)) : 0];
+            const uint8_t* ivb = s_inv + p * TILE * kInvStride + lane * kInvStride;
+            const uint4 hd = s_hdesc[ti & 0xff];
+            const uint32_t* ivw = reinterpret_cast<const uint32_t*>(ivb);
+            uint32_t have = 0;                                         // bit k: inventory[k] > 0
+#pragma unroll
+            for (int w = 0; w < 8; ++w) have |= byte_tops(nonzero_bytes(ivw[w])) << (4 * w);
+            uint32_t cleared = 0;                                      // bit j: listed cell j cleared
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const uint32_t c = ((j < 4 ? cw0 : cw1) >> (8 * (j & 3))) & 0xffu;
+              cleared |= (uint32_t)(c != 0xffu && gr[c != 0xffu ? c : 0u] == 0) << j;
+            }
+            if (live_env && ((ag >> 25) & 1u)) {
               w_label = -1;                                            // frozen: the label of a done env
-            } else if ((ag >> 24) & 1u) {
-              const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
-              const uint8_t* gr = s_grid + p * TILE * GS + lane * GS;
-              const int facing = gr[(x + dir_dx(dir)) * H + (y + dir_dy(dir))];
+            } else if (live_env) {
               int err = 0, kind = 0;
-#if defined(RT_ABL) && (RT_ABL & 1)                                   // ablation builds only: no walk
-              w_label = CRAFT_STOP + (facing & 0);
-#else
-              w_label = hint_leaf(s_task, s_tsub, s_inv + p * TILE * kInvStride + lane * kInvStride, facing,
-                                  (int)(ti & 0xff), err, kind);
-#endif
+              // the hint walk (find_incomplete_subtask): its table, the leaf for this task's
+              // predicate values (craft_host.h hint_tables), or the walk itself
+              if (hd.z & craft_host::kHintWalk) {
+                w_label = hint_leaf(s_task, s_tsub, ivb, facing, (int)(ti & 0xff), err, kind);
+              } else {
+                uint32_t bits = 0;
+#pragma unroll
+                for (int j = 0; j < craft_host::kHintPreds; ++j) {
+                  const uint32_t b = ((j < 4 ? hd.x : hd.y) >> (8 * (j & 3))) & 0xffu;
+                  const uint32_t kd = b & 0x3fu;
+                  const uint32_t t = (b & 0x40u) ? (uint32_t)(facing == (int)kd) : (have >> (kd & 31u)) & 1u;
+                  bits |= ((b >> 7) & t) << j;
+                }
+                const uint32_t lf = s_hleaf[hd.z + bits];
+                if (lf == craft_host::kHintErr) { w_label = -2; err = CRAFT_ETEACHER; }
+                else if (lf == craft_host::kHintStop) w_label = CRAFT_STOP;
+                else if (lf == craft_host::kHintUse) w_label = CRAFT_USE;
+                else { w_label = kTeachGo; kind = (int)lf; }
+              }
               if (err) latch_error(v.err, err, (int64_t)u * TILE + lane);
               w_key = (uint32_t)(x * H + y - H) | ((uint32_t)dir << 8) | ((uint32_t)(kind & 0xff) << 12) |
                       (((ti >> 8) & 1u) << 20);
               if (w_label == kTeachGo) {
                 // the table's row for this grid: the pool row minus the listed cells it cleared
+                // (tt_index), when those are all the cells it cleared
                 const int ncl = (int)(ag >> 26);
-                const int trow = v.ttab && a.use_table && ncl < 63
-                                     ? tt_index(v, (int)(ti >> 10), s_tcell[2 * lane], s_tcell[2 * lane + 1], ncl,
-                                                [&](int c) { return gr[c] == 0; })
-                                     : -1;
+                const int trow = v.ttab && a.use_table && ncl == __popc(cleared)
+                                     ? (int)(ti >> 10) * v.tt_nsub + (int)cleared : -1;
                 const int sl = trow >= 0 ? tt_slot_of(v, kind) : -1;
                 w_need = sl >= 0 ? 1 : 2;
 #if defined(RT_ABL) && (RT_ABL & 2)                                   // ablation: no table loads
@@ -916,7 +1026,9 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             const bool any_req = __ballot(req != ~0u) != 0;          // (the whole wave votes)
             if (lane < TILE) s_treq[q * TILE + lane] = req;
             if (lane == 0) s_tpend[q] = any_req ? (uint32_t)row : ~0u;
+            const uint64_t tf = RT_CLK();
             fetch(q, req);
+            RT_ACC(1, tf);
           }
           duty = D_WALK_JOBS;
           break;
@@ -953,10 +1065,18 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         default:
           break;
       }
+      if (!wait && duty0 == D_WALK) RT_ACC(2, tt);
+      if (!wait && duty0 == D_WALK_JOBS) RT_ACC(4, tt);
       if (duty == D_EXIT) break;
       if (wait) {
-        if (busy()) {
+        const uint64_t ts = RT_CLK();
+        const bool was_busy = busy();
+        if (was_busy) {
           step();
+          RT_ACC(5, ts);
+#ifdef CRAFT_STAMPS
+          if (lane == 0) __hip_atomic_fetch_add(&stt[7], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
           idle_spins = 0;
           if (++steps_run > (1u << 22)) {                              // never hang the GPU (~2 s)
             latch_error(v.err, CRAFT_EINVARIANT, rt_where(5, gbase + (uint32_t)i, (uint32_t)duty));
@@ -964,6 +1084,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           }
         } else {
           __builtin_amdgcn_s_sleep(1);
+          RT_ACC(6, ts);
           if (++idle_spins > kRtSpinCap) {                             // never hang the GPU
             latch_error(v.err, CRAFT_EINVARIANT,
                         rt_where(4, gbase + (uint32_t)i, ((uint32_t)duty << 24) | s_rows[((gbase + i) & (kRtRows - 1)) * RW]));
@@ -974,6 +1095,16 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     }
   }
 
+#ifdef CRAFT_STAMPS
+  if (wave == 0 && lane == 0) {
+    stt[6] = __builtin_amdgcn_s_memrealtime() - st_r0;
+    stt[7] = __builtin_amdgcn_s_memtime() - st_c0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (lane < 8 && v.stamps) v.stamps[(int64_t)blockIdx.x * 64 + wave * 8 + lane] = stt[lane];
+#endif
+#undef RT_CLK
+#undef RT_ACC
   if (tid == 0) {
     unsigned long long* srow = reinterpret_cast<unsigned long long*>(v.stats_part + 4 * (int64_t)blockIdx.x);
     atomicAdd(srow + 0, (unsigned long long)n_succ);

@@ -11,7 +11,11 @@ static hipError_t launch_rt_one(const SimView& v, const RolloutArgs& a, hipStrea
   constexpr int TILE = rt_tile(WIN);
   const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
   if (tiles == 0 || a.n_ticks == 0) return hipSuccess;
+#ifdef CRAFT_STAMPS
+  const size_t lds = (size_t)rt_lds(TILE, v.GS, v.F, NW).bytes + 512;     // + the stamp sums
+#else
   const size_t lds = (size_t)rt_lds(TILE, v.GS, v.F, NW).bytes;
+#endif
   auto kern = rollout_teach_kernel<WIN, TILE, NW>;
   {
     const hipError_t e = ensure_lds<&rollout_teach_kernel<WIN, TILE, NW>>(lds);

@@ -147,6 +147,7 @@ struct craft_sim {
   uint4* d_mask = nullptr;
   uint16_t* d_task = nullptr;
   int32_t* d_task_sub = nullptr;
+  uint32_t* d_hint = nullptr;       // hint_tables: descriptors + leaf bytes
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   uint16_t* d_ttab = nullptr;       // the teacher table (craft_teach.h), or null
@@ -391,6 +392,12 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   std::vector<uint16_t> task_tab(CRAFT_MAX_TASKS, 0);
   std::vector<int32_t> task_sub(CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS, 0);
   craft_host::task_tables(*cfg, task_tab.data(), task_sub.data());
+  std::vector<uint32_t> hint(CRAFT_MAX_TASKS * 4, 0);
+  std::vector<uint8_t> hint_leaf;
+  craft_host::hint_tables(*cfg, task_tab.data(), task_sub.data(), hint.data(), hint_leaf);
+  const size_t hint_bytes = hint.size() * 4 + ((hint_leaf.size() + 15) & ~size_t(15));
+  hint.resize(hint_bytes / 4, 0u);
+  if (!hint_leaf.empty()) memcpy(hint.data() + CRAFT_MAX_TASKS * 4, hint_leaf.data(), hint_leaf.size());
   auto cleanup = [&](hipError_t e, const char* what) {
     fprintf(stderr, "craft_sim_create: %s: %s\n", what, hipGetErrorString(e));
     craft_sim_destroy(s);
@@ -412,6 +419,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_task, sizeof(uint16_t) * task_tab.size());
   ALLOC(s->d_rcw, sizeof(rcw));
   ALLOC(s->d_task_sub, sizeof(int32_t) * task_sub.size());
+  ALLOC(s->d_hint, hint_bytes);
   ALLOC(s->d_stats, 4 * sizeof(int64_t) * s->n_tiles);
   ALLOC(s->d_err, 4 * sizeof(int32_t));
   s->sync_bytes = (16 + 4 * (size_t)((n_envs + 15) / 16) + 15) & ~size_t(15);   // queue + tile_done
@@ -445,6 +453,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     return cleanup(e, "recipe table");
   if ((e = hipMemcpy(s->d_task_sub, task_sub.data(), sizeof(int32_t) * task_sub.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "subtask table");
+  if ((e = hipMemcpy(s->d_hint, hint.data(), hint_bytes, hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "hint table");
 
   SimView& v = s->view;
   v.pool = s->d_pool;
@@ -455,6 +465,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.mask = s->d_mask;
   v.task_tab = s->d_task;
   v.task_sub = s->d_task_sub;
+  v.hint = s->d_hint;
+  v.hint_bytes = (int32_t)hint_leaf.size();
   v.stats_part = s->d_stats;
   v.err = s->d_err;
   v.ttab = nullptr;                       // (until the first pool load: ensure_table)
@@ -557,6 +569,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_task);
   (void)hipFree(s->d_rcw);
   (void)hipFree(s->d_task_sub);
+  (void)hipFree(s->d_hint);
   (void)hipFree(s->d_stats);
   (void)hipFree(s->d_err);
   (void)hipFree(s->d_sync);

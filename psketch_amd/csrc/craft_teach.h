@@ -514,7 +514,10 @@ __device__ __forceinline__ void band_bits(const uint32_t* row32, int nq, int C, 
 // bits 10-12 = first action + 1; bits 0-9 = path length + 1 (-1: no target).
 __device__ __forceinline__ int tt_slot_of(const SimView& v, int kind) {
   if (kind < 0 || kind >= 32) return -1;
-  const int s = (int)((v.tt_slot[kind >> 4] >> (4 * (kind & 15))) & 0xfu);
+  // (a select, not v.tt_slot[kind >> 4]: a per-lane index into the kernel argument would be a
+  // vector load, and its vmcnt(0) would wait for every load the wave has in flight)
+  const uint64_t w = (kind >> 4) ? v.tt_slot[1] : v.tt_slot[0];
+  const int s = (int)((w >> (4 * (kind & 15))) & 0xfu);
   return s == 0xf ? -1 : s;
 }
 __device__ __forceinline__ uint16_t tt_encode(bool ok, int fa, int len) {
