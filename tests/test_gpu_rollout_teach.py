@@ -120,12 +120,13 @@ def test_rollout_teach_hip_equals_cpu_variant(mode):
         assert torch.equal(outs[0][k], outs[1][k]), k
 
 
-def test_rollout_teach_vs_oracle_full_size(oracle_mod):
+@pytest.mark.parametrize("world", ["craft_medium_12x12", "craft_medium_12x12_w5"])
+def test_rollout_teach_vs_oracle_full_size(oracle_mod, world):
     """Config 5's launch (65,536 envs, 40 ticks of hashed actions with auto-reset, every env
-    labelled every tick) against the literal oracle on 256 sampled global ids, run from their
-    initial states with their own ids."""
+    labelled every tick), with 3x3 and 5x5 windows, against the literal oracle on 256 sampled
+    global ids, run from their initial states with their own ids."""
     from oracle import rollout_oracle
-    world, W, n, T, base = "craft_medium_12x12", 12, 65536, 40, 65536
+    W, n, T, base = 12, 65536, 40, 65536
     cfg, pool, specs = _setup(world, W, n, pool_n=1024, seed=0, base=base)
     sim = sim_with_pool(world, n, pool, env_id_base=base)
     sim.reset(*specs)
@@ -217,5 +218,37 @@ def test_rollout_teach_graph_replay():
             assert torch.equal(ra[k], rb[k]), (k, rep)
         a.rollout_teach(K, seed=1, tick0=0, **ra)                # eager between replays
         b.rollout_teach(K, seed=1, tick0=0, **rb)
+    a.check()
+    b.check()
+
+
+def test_rollout_teach_hint_walk_fallback():
+    """A hint tree with more satisfies() predicates than the tabulated walk takes (make[ladder]
+    over bed, axe and shears: 15) keeps the walk itself; mixed with tabulated tasks in one tile,
+    labels equal craft_step_teach's (teach_env's walk) tick by tick."""
+    import copy
+    from psketch_amd import gamedef
+    hints = copy.deepcopy(gamedef.HINTS)
+    hints["make[ladder]"] = ["make[bed]", "make[axe]", "make[shears]", "makeat[workshop2]"]
+    world, W, n, T = "craft_medium_12x12", 12, 4096, 30
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 256)
+    a = CraftSim(world, n_envs=n, device=0, pool_capacity=len(pool), hints=hints)
+    b = CraftSim(world, n_envs=n, device=0, pool_capacity=len(pool), hints=hints)
+    for s in (a, b):
+        s.load_pool(pool)
+    ids = [t.id for t in a.task_manager.dataset_tasks()]
+    ladder = a.task_manager["make[ladder]"].id
+    specs = synthetic_specs(pool, W, W, n, 0, seed=4, task_ids=[ladder, ladder] + ids)
+    a.reset(*specs)
+    b.reset(*specs)
+    out = _rings(a, T)
+    a.rollout_teach(T, seed=2, **out)
+    ob = torch.empty((n, a.n_features), dtype=torch.float32, device="cuda")
+    lb = torch.empty(n, dtype=torch.int32, device="cuda")
+    for t in range(T):
+        b.step(None, seed=2, tick=t, obs=ob, labels=lb)
+        assert torch.equal(out["labels"][t], lb), t
+    assert (host(out["labels"])[:, np.asarray(specs[4]) == ladder] >= 0).mean() > 0.5
     a.check()
     b.check()

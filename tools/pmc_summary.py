@@ -23,7 +23,11 @@ def main(src, dst):
     stats_csv = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats_csv, os.path.join(dst, "kernel_stats.csv"))
     stats = list(csv.DictReader(open(stats_csv)))
-    name = max(stats, key=lambda r: float(r["TotalDurationNs"]))["Name"]
+    # the bench line's kernel (its name up to the first " (" note), else the longest in total; a
+    # one-off setup kernel (the teacher table's build) can outlast a short timed region
+    want = line.get("roofline", {}).get("kernel", "").split(" (")[0].split("<")[0]
+    named = [r for r in stats if want and want in r["Name"]]
+    name = max(named or stats, key=lambda r: float(r["TotalDurationNs"]))["Name"]
     top = next(r for r in stats if r["Name"] == name)
     # per-launch durations from the trace: the first launch is the warmup's when it ran fewer ticks
     trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
