@@ -16,13 +16,13 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(*args):
+def _bench(*args, timeout=240):
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "5",
                           "--no-cpu-baseline", *args], cwd=REPO, env=env, capture_output=True,
-                         text=True, timeout=240)
+                         text=True, timeout=timeout)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
@@ -43,6 +43,21 @@ def test_two_ranks_on_one_card_equal_one_process():
     assert sum(r["episodes"]["env_steps"] for r in d2["ranks"]) == one["episodes"]["env_steps"]
     assert (sum(r["episodes"]["successes"] for r in d2["ranks"]) ==
             d1["ranks"][0]["episodes"]["successes"])
+
+
+def test_eight_ranks_on_one_card_equal_one_process():
+    """The 8-GPU node's shape rehearsed on one card: 8 ranks (gloo) of 8,192 envs each, rank r
+    simulating global ids [r * 8192, (r + 1) * 8192), reduce to the same episode summary as one
+    process simulating all 65,536 (the N=8 scaling line's work split)."""
+    eight = _bench("--gpus", "8", "--one-device", "--dist-backend", "gloo", "--envs", "8192", timeout=420)
+    one = _bench("--gpus", "1", "--envs", "65536")
+    assert eight["n_gpus"] == 8 and eight["config"]["global_batch"] == 65536
+    assert eight["episodes"] == one["episodes"]
+    d8 = eight["dist"]
+    assert d8["backend"] == "gloo" and d8["world_size"] == 8 and len(d8["per_rank_s"]) == 8
+    assert [r["env_id_base"] for r in d8["ranks"]] == [8192 * r for r in range(8)]
+    assert all(r["envs"] == 8192 for r in d8["ranks"])
+    assert sum(r["episodes"]["env_steps"] for r in d8["ranks"]) == one["episodes"]["env_steps"]
 
 
 _RCCL_ONE_RANK = r"""

@@ -252,3 +252,47 @@ def test_rollout_teach_hint_walk_fallback():
     assert (host(out["labels"])[:, np.asarray(specs[4]) == ladder] >= 0).mean() > 0.5
     a.check()
     b.check()
+
+
+@pytest.mark.parametrize("table", [1, 2])
+def test_rollout_teach_late_episode_vs_oracle(oracle_mod, table):
+    """Config 5's size through a whole 40-tick episode in rollout_teach launches ending at ticks
+    9, 25 and 38, USE raised so that cleared cells and crafted inventories are common late in the
+    episode; 1024 envs' labels of those ticks against the literal BFS oracle on the state the
+    launch left, with the teacher table read (1) and off (2)."""
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 512)
+    n, T = 65536, 40
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=12, task_ids=[t.id for t in tm.dataset_tasks()])
+    sim = sim_with_pool(world, n, pool)
+    sim.tune_teach(0, 0, table)
+    sim.reset(*specs)
+    rng = np.random.RandomState(21)
+    acts = torch.as_tensor(rng.choice(6, size=(T, n), p=[.15, .15, .15, .15, .38, .02]).astype(np.int32),
+                           device="cuda")
+    o = oracle_mod.Oracle(cfg, pool)
+    pick = np.random.RandomState(4).choice(n, 1024, replace=False)
+    out = _rings(sim, 16)
+    checked, t0 = 0, 0
+    for t1 in (10, 26, 39, 40):
+        sim.rollout_teach(t1 - t0, seed=5, tick0=t0, actions=acts[t0:t1], autoreset=False, **out)
+        t = t1 - 1
+        t0 = t1
+        if t not in (9, 25, 38):
+            continue
+        st = {k: host(v) for k, v in sim.get_state().items()}
+        sim.check()
+        lh = host(out["labels"][t % 16])
+        cleared = (st["grid"][pick] != pool[st["spec"][pick, 0]]).any(1)
+        if t >= 25:
+            assert cleared.mean() > 0.2 and (st["inventory"][pick][:, 12:].sum(1) > 0).any(), t
+        for i in pick:
+            x, y, d, _ = st["agent"][i]
+            if lh[i] == -1:                                              # frozen: the episode ended
+                continue
+            env = o.env(st["grid"][i], x, y, d, st["inventory"][i])
+            rc, act = o.teacher(env, int(specs[4][i]))
+            assert (rc == 0 and act == lh[i]) or (rc != 0 and lh[i] == -2), (t, i)
+            checked += 1
+    assert checked > 1024
