@@ -536,16 +536,16 @@ template <class Cleared>
 __device__ __forceinline__ int tt_index(const SimView& v, int scen, uint32_t w0, uint32_t w1, int ncl,
                                         Cleared cleared) {
   if (!v.ttab) return -1;
-  int sub = 0, hit = 0;
+  // (cleared() of every slot unconditionally, an unused slot asking cell 0: reads of the grid are
+  // then issued together instead of one round trip each)
+  int sub = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint32_t c = ((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 0xffu;
-    if (c != 0xffu && cleared((int)c)) {
-      sub |= 1 << j;
-      ++hit;
-    }
+    const bool cl = cleared((int)(c != 0xffu ? c : 0u));
+    sub |= (c != 0xffu && cl) ? 1 << j : 0;
   }
-  return hit == ncl ? scen * v.tt_nsub + sub : -1;
+  return __popc((uint32_t)sub) == ncl ? scen * v.tt_nsub + sub : -1;
 }
 // tt_index over a cleared-cell mask m (8 words, 256 cells).
 __device__ __forceinline__ int tt_index_mask(const SimView& v, int scen, uint32_t w0, uint32_t w1,

@@ -65,7 +65,7 @@ class RolloutInfo:
 
 
 def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_obs=False,
-               timing=None, fused_teacher=True, lookahead=False, graph=0):
+               timing=None, fused_teacher=True, lookahead=False, graph=0, graph_key=None):
     """One rollout of sim.n_envs episodes.
 
     spec: (scenario, x, y, dir, task), each n_envs ints (device or host).
@@ -99,10 +99,16 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
       no-ops and are discarded.  The rollout's buffers are the simulator's own: the results are
       copies, and receive() is called once per real tick after the loop, in tick order, with
       rows of a copy of the labels.  Not with keep_obs.
+    graph_key: a hashable naming what the captured graphs read besides the simulator (the
+      student's state); the graphs are reused only while act is the same callable and the key is
+      equal, and captured anew otherwise.  A student that re-allocates a tensor act reads (a
+      new weight tensor instead of an in-place update) must change the key, e.g.
+      tuple(p.data_ptr() for p in model.parameters()), or call drop_graphs(sim): a replay would
+      read the old allocation.
     """
     if graph:
         return _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, timing,
-                              fused_teacher, int(graph))
+                              fused_teacher, int(graph), graph_key)
     t_start = time.perf_counter()
     n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
     if T <= 0:
@@ -234,8 +240,14 @@ def _bc_mask(behavior_clone, n, dev):
     return (bc.reshape(n) != 0).to(torch.uint8).contiguous()
 
 
+def drop_graphs(sim):
+    """Forget the HIP graphs do_rollout(graph=G) captured for `sim` (the next graph rollout
+    captures again): after the student re-allocated a tensor its act reads."""
+    sim._graph_state = None
+
+
 def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, timing,
-                   fused_teacher, G):
+                   fused_teacher, G, graph_key=None):
     """do_rollout(graph=G): see do_rollout."""
     t_start = time.perf_counter()
     n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
@@ -253,10 +265,11 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
     if not flag_dev:
         raise RuntimeError("graph mode needs the any-live flags in mapped host memory")
     gs = getattr(sim, "_graph_state", None)
-    if gs is None or not _same_act(gs["act"], act) or gs["key"] != (is_eval, G, T):
+    key = (is_eval, G, T, graph_key)
+    if gs is None or not _same_act(gs["act"], act) or gs["key"] != key:
         sim._graph_state = None                  # drop the old graphs before capturing new ones
         gs = sim._graph_state = {
-            "act": _weak_act(act), "key": (is_eval, G, T), "graphs": [],
+            "act": _weak_act(act), "key": key, "graphs": [],
             "obs": sim.empty_obs(), "success": torch.zeros(n, dtype=torch.int8, device=dev),
             "seqs": torch.full((T, n), -1, dtype=torch.int32, device=dev),
             "refs": None if is_eval else torch.empty((T + 1, n), dtype=torch.int32, device=dev),

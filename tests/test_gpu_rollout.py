@@ -313,3 +313,54 @@ def test_do_rollout_raises_where_the_reference_raises(golden, gpu, case):
     with pytest.raises(RolloutError, match="None" if case == "none_success" else "len\\(None\\)"):
         do_rollout(sim, spec, lambda obs, t: stop, True)
     sim.check()                                           # nothing latched besides the flags
+
+
+def test_graph_rollout_student_reallocates_weights(gpu):
+    """A student that replaces its weight tensor (a new allocation, as an optimizer that
+    rebinds parameters does) between rollouts: with graph_key naming the allocation the graphs
+    are captured anew and the rollout equals the synchronous loop's with the new weights; with
+    the key unchanged, drop_graphs(sim) does the same.  (A replay of the old capture would read
+    the old tensor.)"""
+    from psketch_amd import CraftSim
+    from psketch_amd.rollout import do_rollout, drop_graphs
+    from psketch_amd.sim import sample_scenarios, synthetic_specs
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 128)
+    n = 8192
+    rng = np.random.RandomState(9)
+
+    class Student:
+        def __init__(self):
+            self.W = torch.as_tensor(rng.randint(-3, 4, size=(cfg.n_features, 6)).astype(np.float64), device=gpu)
+
+        def act(self, obs, t):
+            return (obs.double() @ self.W).argmax(dim=1).to(torch.int32)
+
+    st = Student()
+    spec = synthetic_specs(pool, 12, 12, n, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
+    bc = rng.binomial(1, 0.5, size=n)
+    ref_sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    g_sim = CraftSim(world, n_envs=n, device=gpu.index, pool_capacity=len(pool))
+    for s in (ref_sim, g_sim):
+        s.load_pool(pool)
+
+    def both(key, before=None):
+        a = do_rollout(ref_sim, spec, st.act, False, behavior_clone=bc)
+        if before:
+            before()
+        b = do_rollout(g_sim, spec, st.act, False, behavior_clone=bc, graph=8, graph_key=key)
+        for k in ("action_seqs", "n_actions", "success", "distances"):
+            assert torch.equal(getattr(a, k), getattr(b, k)), k
+        return g_sim._graph_state["graphs"]
+
+    g0 = both((st.W.data_ptr(),))
+    keep = st.W                                     # the old allocation stays alive (no reuse)
+    st.W = torch.flip(keep, dims=[1]).contiguous()  # new weights in a new tensor
+    g1 = both((st.W.data_ptr(),))
+    assert g1 is not g0                             # captured anew for the new key
+    st.W = torch.roll(keep, 1, dims=1).contiguous()
+    g2 = both(None, before=lambda: drop_graphs(g_sim))
+    assert g2 is not g1
+    assert both(None) is g2                         # same act and key: the graphs are reused
+    del keep
