@@ -62,8 +62,8 @@ struct SimView {
   int32_t tt_slots;
   int32_t tt_nsub;            // 1 << tt_m
   int32_t tt_fused;           // 1: the fused tick + teacher kernels read the table too (set per
-                              // launch by craft_step_teach, CRAFT_TT_FUSED; 0: they defer every
-                              // go[X] BFS instead)
+                              // launch by craft_step_teach from craft_sim_tune_teach's table mode;
+                              // 0: they defer every go[X] BFS instead)
   uint64_t tt_slot[2];
   uint64_t kc_lo, kc_hi;      // kind class, 4 bits per kind id
   // compact recipes, 3 words each: out | ws<<8 | n_in<<16 | kind0<<24, count0 | kind1<<8 |

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Every bench line of the round on one box (no profiler attached), one JSON file each in $OUT:
 # the driver's command, 512 steps, the one-tick kernel (16-slot ring and one reused buffer),
-# config 5 (fused teacher), the closed-loop trainer, the w = 5 rollout and one-tick lines, and
-# config 5 at w = 5.
+# config 5 (teacher-labelled K-tick launches at K = 32 and 20, and the one-tick fused kernel),
+# the closed-loop trainer, the w = 5 rollout and one-tick lines, and config 5 at w = 5.
 set -u
 REPO="${GRAFT_REPO_ROOT:-/root/repo}"
 OUT="$REPO/gpurun_out/${TAG:-lines}"
@@ -19,7 +19,9 @@ run steps512 --steps 512 --warmup 5
 run k1 --ticks-per-launch 1 --steps 200 --warmup 20
 run k1_ring1 --ticks-per-launch 1 --ring 1 --steps 200 --warmup 20
 run config5 --workload teacher --steps 200 --warmup 20
+run config5_k20 --workload teacher --ticks-per-launch 20 --steps 200 --warmup 20
+run config5_k1 --workload teacher --ticks-per-launch 1 --steps 200 --warmup 20
 run trainer --workload trainer --steps 5 --warmup 2
 run w5 --world craft_medium_12x12_w5 --steps 20 --warmup 5
 run w5_k1 --world craft_medium_12x12_w5 --ticks-per-launch 1 --steps 100 --warmup 10
-run config5_w5 --world craft_medium_12x12_w5 --workload teacher --steps 100 --warmup 10
+run config5_w5 --world craft_medium_12x12_w5 --workload teacher --ticks-per-launch 20 --steps 100 --warmup 10
