@@ -175,10 +175,13 @@ int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t thread
  *           windows and the default tile only; otherwise the one-tile kernel);
  *   lanes   teacher lanes per query: 0 (default) = each kernel's measured best; 1, 2 or 4 for
  *           craft_teacher and the one-tile kernel, 2 or 4 for the two-tile kernel (others: 2);
- *   table   which teachers read the teacher table (find_closest_resources answered when a pool
- *           row is loaded, for every go/get target kind, start cell and direction: 4*W*H u16
- *           entries per kind per pool row, allocated at craft_sim_create for pool_capacity rows
- *           when they fit in 1 GiB), for envs that have cleared no cell: 0 (default) = auto
+ *   table   which teachers read the teacher table (find_closest_resources answered ahead of
+ *           time for every grid an env can reach: its pool row minus any subset of the row's
+ *           first m clearable cells (m <= 8), for every go/get target kind, start cell and
+ *           direction; 4*W*H u16 entries per kind per (row, subset), allocated at the first pool
+ *           load for pool_capacity rows with m chosen to fit 1 GiB (12x12 craft_medium: m = 6,
+ *           453 MB for 1024 rows); a loaded row's entries are built by the next launch that reads
+ *           the table, on its stream), for envs whose grid it lists: 0 (default) = auto
  *           (craft_step_teach only when its launch rewrites the previous launch's observation
  *           buffer, where the reads hit the Infinity Cache; every other teacher always),
  *           1 = always, 2 = never (every query runs the BFS). */

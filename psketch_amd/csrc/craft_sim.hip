@@ -154,6 +154,9 @@ struct craft_sim {
   uint32_t* d_ttcells = nullptr;    // [pool_capacity][2]: each row's listed clearable cells
   int tt_nslot = 0;                 // target-kind slots of the table
   bool tt_decided = false;          // its size is fixed at the first pool load (ensure_table)
+  // pool rows loaded since the table was last built: craft_pool_load only records them, and the
+  // next launch that reads the table builds their entries first, on its own stream
+  std::vector<std::pair<int32_t, int32_t>> tt_dirty;
   // craft_sim_tune_teach: which teacher reads the table (0 auto: craft_step_teach when the launch
   // rewrites the previous launch's observation buffer, as a trainer's loop does, every other
   // teacher always; 1 always; 2 never), and teacher lanes per query (0 = each kernel's default)
@@ -274,6 +277,20 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
   const int tl1 = (s->teach_lanes == 1 || s->teach_lanes == 2) ? s->teach_lanes : 4;
   if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
   else { *kernel = 1; *envs = craft::kMaxTileEnvs; *lanes = tl1; }
+}
+
+// Builds the teacher-table entries (and listed clearable cells) of the rows loaded since the last
+// build, on `stream`, ahead of the launch about to read them.
+hipError_t flush_table(craft_sim* s, void* stream) {
+  if (s->tt_dirty.empty()) return hipSuccess;
+  if (s->d_ttab)
+    for (const auto& r : s->tt_dirty) {
+      const hipError_t e = craft::launch_teach_table(craft::teach_words(s->view.W, s->view.H), s->view, r.first,
+                                                     r.second, s->tt_kinds, reinterpret_cast<hipStream_t>(stream));
+      if (e != hipSuccess) return e;
+    }
+  s->tt_dirty.clear();
+  return hipSuccess;
 }
 
 // The view a teacher launch gets: the table hidden when craft_sim_tune_teach says never.
@@ -651,10 +668,11 @@ int craft_pool_load(craft_sim_t* s, const uint8_t* grids, int32_t first, int32_t
     ensure_table(s, maxm);
     HIP_TRY(s, hipMemcpy(s->d_pool + (size_t)first * CS, staged.data(), staged.size(), hipMemcpyHostToDevice));
     HIP_TRY(s, hipMemcpy(s->d_pool_conn + first, conn.data(), count, hipMemcpyHostToDevice));
-    // the rows' teacher-table entries (synchronous, like the load itself)
-    HIP_TRY(s, craft::launch_teach_table(craft::teach_words(s->view.W, s->view.H), s->view, first, count,
-                                         s->tt_kinds, nullptr));
-    HIP_TRY(s, hipStreamSynchronize(nullptr));
+    // the rows' teacher-table entries: built by the next launch that reads the table (flush_table)
+    if (!s->tt_dirty.empty() && s->tt_dirty.back().first + s->tt_dirty.back().second == first)
+      s->tt_dirty.back().second += count;
+    else
+      s->tt_dirty.emplace_back(first, count);
   }
   if (first + count > s->pool_count) s->pool_count = first + count;
   s->view.pool_count = s->pool_count;
@@ -783,6 +801,7 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   // loop: ring 1, -2.5 us per tick) and go to HBM beside the store stream when every launch
   // writes a fresh buffer (a 16-slot ring: +0.5 us), so auto mode reads them only in the first
   // case (profiles/r04/ab5).
+  HIP_TRY(s, flush_table(s, stream));
   SimView v = teach_view(s);
   v.tt_fused = s->teach_table == 1 || (s->teach_table == 0 && (a.obs == nullptr || a.obs == s->last_teach_obs));
   s->last_teach_obs = a.obs;
@@ -935,6 +954,7 @@ int craft_rollout_teach(craft_sim_t* s, const craft_rollout_teach_args_t* x, voi
   }
   int64_t grid = 0;
   a.grid_out = &grid;
+  HIP_TRY(s, flush_table(s, stream));
   SimView v = teach_view(s);
   v.obs_policy = s->rollout_obs_policy;
   const int64_t units = (s->n_envs + craft::rt_tile_of(s->cfg.window_width) - 1) / craft::rt_tile_of(s->cfg.window_width);
@@ -996,6 +1016,7 @@ int craft_rollout_distances(craft_sim_t* s, const int32_t* tasks, const int8_t* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(s, hipMemsetAsync(flags_out, 0, 2 * sizeof(int32_t), st));
   if (s->n_envs == 0) return CRAFT_OK;
+  HIP_TRY(s, flush_table(s, stream));
   hipError_t e = craft::launch_distances(craft::teach_words(s->view.W, s->view.H), teach_view(s), tasks, success, action_seqs, ticks,
                                          s->n_envs, distances_out, is_get_out, n_actions_out, flags_out, st);
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout_distances launch");
@@ -1011,6 +1032,7 @@ int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
   if (4 * s->view.C > 1000)
     return fail(s, CRAFT_EINVAL, "craft_teacher: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
   if (n == 0) return CRAFT_OK;
+  HIP_TRY(s, flush_table(s, stream));
   hipError_t e = craft::launch_teacher(craft::teach_words(s->view.W, s->view.H), s->teach_lanes, teach_view(s), slots, tasks, n, action_out,
                                        path_len_out, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_teacher launch");
