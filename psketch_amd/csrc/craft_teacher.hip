@@ -228,7 +228,8 @@ __global__ __launch_bounds__(256) void distances_kernel(SimView v, DistArgs a) {
     }
   }
   if (lead) {
-    int na = 0;
+    int na = 0;                          // (8 loads in flight at a time, not one)
+#pragma unroll 8
     for (int t = 0; t < a.ticks; ++t) na += a.seqs[(int64_t)t * a.n + i] >= 0;
     a.dist_out[i] = d;
     a.is_get_out[i] = is_get;

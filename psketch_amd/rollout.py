@@ -277,7 +277,8 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
     obs, success, seqs, refs = gs["obs"], gs["success"], gs["seqs"], gs["refs"]
     sim.reset(*spec, obs=obs)
     success.zero_()
-    seqs.fill_(-1)
+    # (every tick writes its whole action-record row; rows past the last tick are filled after
+    # the loop, usually none)
     if not is_eval:
         gs["bc"].copy_(_bc_mask(behavior_clone, n, dev))
         sim.teacher(action_out=refs[0])          # the initial states' labels; then every step's
@@ -329,6 +330,8 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
         c += 1
         if ticks is None and c >= nch:
             ticks = T
+    if ticks < T:
+        seqs[ticks:].fill_(-1)
     if not is_eval and receive is not None:
         labels = refs[:ticks].clone()
         for t in range(ticks):

@@ -296,3 +296,27 @@ def test_rollout_teach_late_episode_vs_oracle(oracle_mod, table):
             assert (rc == 0 and act == lh[i]) or (rc != 0 and lh[i] == -2), (t, i)
             checked += 1
     assert checked > 1024
+
+
+def test_rollout_teach_refusals_on_the_gpu():
+    """The HIP library refuses what the CPU variant refuses (tests/test_rollout_teach_cpu.py):
+    labels feeding actions without label_in, a ring shorter than one slot, negative ticks; a
+    refused call launches nothing and leaves the states as they were."""
+    from psketch_amd import _native as N
+    world, W, n = "craft_medium_12x12", 12, 256
+    cfg, pool, specs = _setup(world, W, n, pool_n=16)
+    sim = sim_with_pool(world, n, pool)
+    sim.reset(*specs)
+    before = {k: v.clone() for k, v in sim.get_state().items()}
+    with pytest.raises(N.CraftError):
+        sim.rollout_teach(4, label_actions=True)
+    with pytest.raises(N.CraftError):
+        sim.rollout_teach(4, behavior_clone=torch.ones(n, dtype=torch.uint8, device="cuda"))
+    with pytest.raises(N.CraftError):
+        sim.rollout_teach(4, tick0=-1)
+    with pytest.raises(N.CraftError):
+        sim.tune_teach(0, 3, 0)
+    after = sim.get_state()
+    for k in before:
+        assert torch.equal(before[k], after[k]), k
+    sim.check()
