@@ -524,12 +524,15 @@ def run(args):
         if world_size == 1 and not args.no_cpu_baseline:
             c_leg = cpu_baseline_c(sim.config, grids, specs, env_base, args.seed, args.cpu_seconds,
                                    teacher=teacher)
-            try:
-                np_leg = cpu_baseline_numpy(sim.config, grids, specs, env_base, args.seed,
-                                            args.cpu_seconds)
-            except Exception as e:          # the C leg stands alone if process pools are refused
-                np_leg = {"error": f"{type(e).__name__}: {e}"}
-            line["cpu_baseline"] = dict(c_leg, python_numpy=np_leg)
+            if teacher:                     # the numpy restatement has no teacher: no like-for-like leg
+                np_leg = None
+            else:
+                try:
+                    np_leg = cpu_baseline_numpy(sim.config, grids, specs, env_base, args.seed,
+                                                args.cpu_seconds)
+                except Exception as e:      # the C leg stands alone if process pools are refused
+                    np_leg = {"error": f"{type(e).__name__}: {e}"}
+            line["cpu_baseline"] = dict(c_leg, **({"python_numpy": np_leg} if np_leg is not None else {}))
         print(json.dumps(line), flush=True)
     D.shutdown()
 

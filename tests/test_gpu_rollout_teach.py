@@ -320,3 +320,24 @@ def test_rollout_teach_refusals_on_the_gpu():
     for k in before:
         assert torch.equal(before[k], after[k]), k
     sim.check()
+
+
+@pytest.mark.parametrize("n", [1, 7, 33, 95])
+def test_rollout_teach_tiny_batches_equal_cpu_variant(n):
+    """Fewer envs than one tile, one env past a tile, three tiles minus one: the persistent grid
+    sizes itself to the tiles and the tail tile's idle lanes store nothing."""
+    world, W, T = "craft_medium_12x12", 12, 30
+    cfg, pool, specs = _setup(world, W, n, pool_n=16, seed=n)
+    g = sim_with_pool(world, n, pool)
+    c = CraftSim(world, n_envs=n, device="cpu", pool_capacity=len(pool))
+    c.load_pool(pool)
+    outs = []
+    for s in (g, c):
+        s.reset(*specs)
+        r = _rings(s, 8)
+        s.rollout_teach(T, seed=4, **r)
+        s.check()
+        outs.append(({k: v.cpu() for k, v in r.items()}, {k: v.cpu() for k, v in s.get_state().items()}))
+    for a, b in zip(*outs):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
