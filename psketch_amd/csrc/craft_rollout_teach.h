@@ -945,7 +945,11 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           w_label = -2;
           w_need = 0;                                                  // 1: a table answer, 2: a BFS job
           uint32_t req = ~0u;                                          // (policy actions) the ttab index asked
+#if defined(RT_ABL) && (RT_ABL & 1)                                   // ablation builds only: no walk
+          if (false) {
+#else
           if (lane < nE) {
+#endif
             // the walk's loads in three rounds, each issued together: the agent and task words and
             // the row's listed clearable cells; the facing cell, the hint descriptor, the inventory
             // and the listed cells' kinds now; the hint leaf
@@ -1009,6 +1013,9 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
                 if (w_need == 2) { w_need = 0; w_label = CRAFT_STOP; }
 #endif
                 if (w_need == 1) req = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
+#if defined(RT_ABL) && (RT_ABL & 16)                                  // ablation: fetch, never decode
+                if (w_need == 1) { w_need = 0; w_label = CRAFT_STOP; }
+#endif
               }
             }
           }
@@ -1025,7 +1032,11 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             if (!lsync) decode_slot(q, false);
             const bool any_req = __ballot(req != ~0u) != 0;          // (the whole wave votes)
             if (lane < TILE) s_treq[q * TILE + lane] = req;
+#if defined(RT_ABL) && (RT_ABL & 16)
+            if (lane == 0) s_tpend[q] = ~0u;
+#else
             if (lane == 0) s_tpend[q] = any_req ? (uint32_t)row : ~0u;
+#endif
             const uint64_t tf = RT_CLK();
             fetch(q, req);
             RT_ACC(1, tf);
@@ -1067,7 +1078,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       }
       if (!wait && duty0 == D_WALK) RT_ACC(2, tt);
       if (!wait && duty0 == D_WALK_JOBS) RT_ACC(4, tt);
-      if (duty == D_EXIT) break;
+      if (duty == D_EXIT) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                // no LDS-DMA outlives the wave
+        break;
+      }
       if (wait) {
         const uint64_t ts = RT_CLK();
         const bool was_busy = busy();
