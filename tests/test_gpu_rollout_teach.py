@@ -341,3 +341,25 @@ def test_rollout_teach_tiny_batches_equal_cpu_variant(n):
     for a, b in zip(*outs):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("fmt", ["bf16", "u8"])
+def test_rollout_teach_obs_formats(fmt):
+    """The narrower observation formats hold the same exact values (craft_sim_set_obs_format):
+    the teacher rollout's ring in bf16 / u8 equals its fp32 ring, labels and states unchanged."""
+    world, W, n, T = "craft_medium_12x12", 12, 4096, 24
+    cfg, pool, specs = _setup(world, W, n, seed=8)
+    outs = []
+    for f in ("f32", fmt):
+        s = sim_with_pool(world, n, pool)
+        s.set_obs_format(f)
+        s.reset(*specs)
+        r = _rings(s, T)
+        s.rollout_teach(T, seed=6, **r)
+        s.check()
+        outs.append(({k: v.float() if k == "obs" else v for k, v in r.items()}, s.get_state()))
+    (a, sa), (b, sb) = outs
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
