@@ -42,7 +42,8 @@ def _setup(world, W, n, pool_n=256, seed=6, base=0):
     ("craft_medium_12x12", 12, 4099, 30, 10, 30, "bc", False),
     ("craft_medium", 8, 3000, 30, 15, 30, "given", True),            # 8x8: two words per cell set
     ("craft_large", 10, 1500, 25, 25, 25, "policy", True),           # 10x10, 5x5 windows
-    ("craft_medium_12x12_w5", 12, 2048, 25, 25, 25, "given", True)])
+    ("craft_medium_12x12_w5", 12, 2048, 25, 25, 25, "given", True),
+    ("craft_medium_12x12", 12, 8192, 30, 15, 30, "given_bc", True)])      # action table + cloning
 def test_rollout_teach_equals_step_teach(world, W, n, T, K, ring, mode, autoreset):
     cfg, pool, specs = _setup(world, W, n)
     a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
@@ -50,8 +51,8 @@ def test_rollout_teach_equals_step_teach(world, W, n, T, K, ring, mode, autorese
     b.reset(*specs)
     rng = np.random.RandomState(11)
     acts = (rng.choice(6, size=(T, n), p=[.18, .18, .18, .18, .26, .02]).astype(np.int32)
-            if mode == "given" else None)
-    bc = (rng.rand(n) < 0.5).astype(np.uint8) if mode == "bc" else None
+            if mode in ("given", "given_bc") else None)
+    bc = (rng.rand(n) < 0.5).astype(np.uint8) if mode in ("bc", "given_bc") else None
     src = (torch.ones(n, dtype=torch.uint8, device="cuda") if mode == "label"
            else (torch.as_tensor(bc, device="cuda") if bc is not None else None))
     cur = b.teacher()[0].clone()                                  # labels of the reset states

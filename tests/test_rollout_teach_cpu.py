@@ -29,7 +29,8 @@ def _run(sim, T, ring, **kw):
 # mode: the action source (policy = hashed draw, given = an action table, bc = behaviour cloning on
 # half the envs, label = every env acts on its label: make_data's demonstrations)
 @pytest.mark.parametrize("mode,autoreset", [("policy", True), ("given", True), ("bc", True),
-                                            ("label", False), ("label", True), ("bc", False)])
+                                            ("label", False), ("label", True), ("bc", False),
+                                            ("given_bc", True)])
 def test_rollout_teach_cpu_vs_oracle(oracle_mod, mode, autoreset):
     from oracle import rollout_oracle
     world = "craft_medium_12x12"
@@ -40,9 +41,10 @@ def test_rollout_teach_cpu_vs_oracle(oracle_mod, mode, autoreset):
     sim = cpu_sim(world, n, pool, env_id_base=base)
     sim.reset(*specs)
     rng = np.random.RandomState(5)
-    acts = rng.choice(6, size=(T, n), p=[.2, .2, .2, .2, .18, .02]).astype(np.int32) if mode == "given" else None
-    bc = (rng.rand(n) < 0.5).astype(np.uint8) if mode == "bc" else None
-    lsrc = mode in ("bc", "label")
+    acts = (rng.choice(6, size=(T, n), p=[.2, .2, .2, .2, .18, .02]).astype(np.int32)
+            if mode in ("given", "given_bc") else None)
+    bc = (rng.rand(n) < 0.5).astype(np.uint8) if mode in ("bc", "given_bc") else None
+    lsrc = mode in ("bc", "label", "given_bc")
     label_in = sim.teacher()[0].clone() if lsrc else None
     out = _run(sim, T, T, seed=seed, actions=None if acts is None else torch.as_tensor(acts),
                autoreset=autoreset, label_in=label_in, behavior_clone=None if bc is None else torch.as_tensor(bc),
