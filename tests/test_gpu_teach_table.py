@@ -77,3 +77,39 @@ def test_rollout_summary_with_and_without_table():
     for k in ("action_seqs", "n_actions", "success", "distances", "is_get"):
         assert torch.equal(getattr(infos[0], k), getattr(infos[1], k)), k
     assert (infos[0].distances > 0).any()
+
+
+def test_table_rows_loaded_piecewise_and_reloaded():
+    """Pool rows loaded in pieces (out of order, one row alone, a row replaced by another grid)
+    and generated on the device: the table entries are built lazily by the next launch that
+    reads the table, so every teacher answers as the table-off BFS does, including for the
+    replaced row."""
+    world, W, n = "craft_medium_12x12", 12, 8192
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 96)
+    other, _, _ = sample_scenarios(params, cb, 7, 1)
+    sims = []
+    for table in (1, 2):
+        s = CraftSim(world, n_envs=n, device=0, pool_capacity=128)
+        s.tune_teach(0, 0, table)
+        s.load_pool(pool[40:96], first=40)
+        s.load_pool(pool[:1], first=0)
+        s.load_pool(pool[1:40], first=1)
+        sims.append(s)
+    specs = synthetic_specs(pool, W, W, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
+    for s in sims:
+        s.reset(*specs)
+    first = [s.teacher()[0].clone() for s in sims]
+    assert torch.equal(first[0], first[1])
+    pool2 = pool.copy()
+    pool2[5] = other[0]
+    specs = synthetic_specs(pool2, W, W, n, 0, seed=2, task_ids=[t.id for t in tm.dataset_tasks()])
+    for s in sims:                                     # row 5 replaced: its entries rebuilt
+        s.load_pool(other, first=5)
+        s.reset(*specs)
+    second = [s.teacher()[0].clone() for s in sims]
+    assert torch.equal(second[0], second[1])
+    rows5 = torch.as_tensor(np.asarray(specs[0]) == 5, device="cuda")
+    assert not torch.equal(first[0][rows5], second[0][rows5])    # (the new grid answers differently)
+    for s in sims:
+        s.check()
