@@ -58,6 +58,11 @@ struct SimView {
   // slot = the target kind's slot (tt_slot: 4 bits per kind id, 0xf = none), subset bit j = the
   // row's clearable cell tt_cells[row] byte j cleared (0xff = no such cell); null when off
   const uint16_t* ttab;
+  // the same answers as the label they give (go_leaf_action), 4 bits each, one tt_blk-byte block
+  // per (trow, slot): entry dir * C + cell in the low (even) / high (odd) nibble of byte >> 1;
+  // 0-3 the first action, 4 STOP (no target), 5 the reference raises, 15 not computed
+  const uint8_t* ttab4;
+  int32_t tt_blk;             // bytes per block: 2 C rounded up to 16
   const uint32_t* tt_cells;   // [P][2]: each row's first tt_m clearable cells, a byte each
   int32_t tt_slots;
   int32_t tt_nsub;            // 1 << tt_m

@@ -80,7 +80,8 @@ constexpr uint32_t kRtSpinCap = 1u << 22;
 // [8][4 + TILE] | BFS job queue [32][2 NW + 1] | table requests [4][TILE] | table words [4][64] |
 // their rows [4] | clearable cells [TILE][2] | hint table: descriptors [64][4], leaf bytes [2048]
 struct RtLds {
-  int pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint, bytes;
+  int pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint, tnib,
+      bytes;
 };
 __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -102,7 +103,8 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.tpend = l.tval + kRtLag * 64 * 4;                      // [kRtLag] their label rows (~0: none)
   l.tcell = l.tpend + kRtLag * 4;                          // [tile][2] each env's listed clearable cells
   l.hint = up16(l.tcell + tile * 8);                       // craft_host.h hint_tables
-  l.bytes = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;
+  l.tnib = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;   // [kRtLag][tile] nibble in the word
+  l.bytes = up16(l.tnib + kRtLag * tile);
   return l;
 }
 // envs per tile: 32 for 3x3 windows (as the split rollout kernel), 16 for wider ones (their
@@ -167,6 +169,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   uint32_t* s_tval = reinterpret_cast<uint32_t*>(smem + lay.tval);    // [kRtLag][64] fetched table words
   uint32_t* s_tpend = reinterpret_cast<uint32_t*>(smem + lay.tpend);  // [kRtLag] their label rows, ~0 none
   uint32_t* s_tcell = reinterpret_cast<uint32_t*>(smem + lay.tcell);  // [TILE][2] tt_cells of the env's row
+  uint8_t* s_tnib = smem + lay.tnib;                                  // [kRtLag][TILE] the answer's nibble
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
@@ -831,9 +834,17 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     // a dummy one when the item asks for none, so that the fetch of the item kRtLag walks back is
     // exactly the one vmcnt(kRtLag - 1) leaves waiting for (loads complete in order; any other
     // VMEM op of this wave, a latched error, only makes the wait stricter).
-    const uint32_t* tbase = reinterpret_cast<const uint32_t*>(v.ttab ? (const void*)v.ttab : (const void*)v.task_tab);
+    // (the answers as 4-bit labels, SimView::ttab4: a quarter of the u16 table's footprint, so
+    // more of the lines the gather touches are L2 hits; req is then the dword index)
+#ifdef RT_U16_GATHER
+    const bool nib = false;
+#else
+    const bool nib = v.ttab4 != nullptr;
+#endif
+    const uint32_t* tbase = reinterpret_cast<const uint32_t*>(
+        nib ? (const void*)v.ttab4 : v.ttab ? (const void*)v.ttab : (const void*)v.task_tab);
     auto fetch = [&](int q, uint32_t req) __attribute__((always_inline)) {
-      const uint32_t* gp = tbase + (req == ~0u ? 0u : req >> 1);
+      const uint32_t* gp = tbase + (req == ~0u ? 0u : nib ? req : req >> 1);
       const uint32_t lds = __builtin_amdgcn_readfirstlane(
           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(s_tval + q * 64));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // the slot's last reads are done
@@ -854,11 +865,18 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       const uint32_t req = lane < TILE ? s_treq[q * TILE + lane] : ~0u;
       if (req != ~0u) {
         const uint32_t word = s_tval[q * 64 + lane];
-        const uint32_t val = (req & 1u) ? word >> 16 : word & 0xffffu;
         int err = 0, label = -2;
-        if (val & 0x8000u) label = go_leaf_action((val & 0x4000u) != 0, (int)((val >> 10) & 7u) - 1,
-                                                  (int)(val & 0x3ffu) - 1, err);
-        else err = CRAFT_EINVARIANT;                                   // (a reachable grid has its entry)
+        if (nib) {
+          const uint32_t code = (word >> (4 * (uint32_t)s_tnib[q * TILE + lane])) & 0xfu;
+          if (code < 4) label = (int)code;
+          else if (code == 4) label = CRAFT_STOP;
+          else err = code == 5 ? CRAFT_ETEACHER : CRAFT_EINVARIANT;  // the reference raises; 15: no entry
+        } else {
+          const uint32_t val = (req & 1u) ? word >> 16 : word & 0xffffu;
+          if (val & 0x8000u) label = go_leaf_action((val & 0x4000u) != 0, (int)((val >> 10) & 7u) - 1,
+                                                    (int)(val & 0x3ffu) - 1, err);
+          else err = CRAFT_EINVARIANT;                                 // (a reachable grid has its entry)
+        }
         R[4 + lane] = (uint32_t)label;
         if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + lane);
       }
@@ -945,6 +963,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           w_label = -2;
           w_need = 0;                                                  // 1: a table answer, 2: a BFS job
           uint32_t req = ~0u;                                          // (policy actions) the ttab index asked
+          uint32_t w_nib = 0;                                          // (nibble table) the nibble in that word
 #if defined(RT_ABL) && (RT_ABL & 1)                                   // ablation builds only: no walk
           if (false) {
 #else
@@ -1012,7 +1031,15 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
 #if defined(RT_ABL) && (RT_ABL & 4)                                   // ablation: no BFS jobs
                 if (w_need == 2) { w_need = 0; w_label = CRAFT_STOP; }
 #endif
-                if (w_need == 1) req = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
+                if (w_need == 1) {
+                  if (nib) {                                           // the dword holding the nibble
+                    const uint32_t idx = (uint32_t)(dir * C + x * H + y);
+                    req = ((uint32_t)trow * (uint32_t)v.tt_slots + (uint32_t)sl) * (uint32_t)(v.tt_blk >> 2) + (idx >> 3);
+                    w_nib = idx & 7u;
+                  } else {
+                    req = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
+                  }
+                }
 #if defined(RT_ABL) && (RT_ABL & 16)                                  // ablation: fetch, never decode
                 if (w_need == 1) { w_need = 0; w_label = CRAFT_STOP; }
 #endif
@@ -1031,7 +1058,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             const int q = (int)(g & (kRtLag - 1));
             if (!lsync) decode_slot(q, false);
             const bool any_req = __ballot(req != ~0u) != 0;          // (the whole wave votes)
-            if (lane < TILE) s_treq[q * TILE + lane] = req;
+            if (lane < TILE) {
+              s_treq[q * TILE + lane] = req;
+              s_tnib[q * TILE + lane] = (uint8_t)w_nib;
+            }
 #if defined(RT_ABL) && (RT_ABL & 16)
             if (lane == 0) s_tpend[q] = ~0u;
 #else

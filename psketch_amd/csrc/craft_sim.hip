@@ -151,6 +151,7 @@ struct craft_sim {
   int64_t* d_stats = nullptr;
   int32_t* d_err = nullptr;
   uint16_t* d_ttab = nullptr;       // the teacher table (craft_teach.h), or null
+  uint8_t* d_ttab4 = nullptr;       // its answers as 4-bit labels (SimView::ttab4)
   uint32_t* d_ttcells = nullptr;    // [pool_capacity][2]: each row's listed clearable cells
   int tt_nslot = 0;                 // target-kind slots of the table
   bool tt_decided = false;          // its size is fixed at the first pool load (ensure_table)
@@ -298,6 +299,7 @@ SimView teach_view(const craft_sim* s) {
   SimView v = s->view;
   if (s->teach_table == 2) {
     v.ttab = nullptr;
+    v.ttab4 = nullptr;
     v.tt_slots = 0;
   }
   return v;
@@ -335,14 +337,20 @@ void ensure_table(craft_sim* s, int max_clearable) {
   if (s->tt_nslot == 0) return;
   const size_t budget = (size_t)1 << 30;
   int m = std::min(8, std::max(0, max_clearable));
+  const size_t blk = ((size_t)2 * C + 15) & ~(size_t)15;      // SimView::tt_blk
   auto bytes = [&](int mm) { return ((size_t)s->pool_capacity << mm) * s->tt_nslot * 4 * C * sizeof(uint16_t); };
-  while (m >= 0 && (bytes(m) > budget || ((int64_t)s->pool_capacity << m) >= ((int64_t)1 << 21))) --m;
+  auto bytes4 = [&](int mm) { return ((size_t)s->pool_capacity << mm) * s->tt_nslot * blk; };
+  while (m >= 0 && (bytes(m) + bytes4(m) > budget || ((int64_t)s->pool_capacity << m) >= ((int64_t)1 << 21))) --m;
   if (m < 0) return;
-  if (hipMalloc(&s->d_ttab, bytes(m)) != hipSuccess) {
+  if (hipMalloc(&s->d_ttab, bytes(m)) != hipSuccess || hipMalloc(&s->d_ttab4, bytes4(m)) != hipSuccess) {
     (void)hipGetLastError();
+    (void)hipFree(s->d_ttab);
     s->d_ttab = nullptr;                  // no table: every query runs the BFS (same results)
+    s->d_ttab4 = nullptr;
     return;
   }
+  s->view.ttab4 = s->d_ttab4;
+  s->view.tt_blk = (int32_t)blk;
   s->view.ttab = s->d_ttab;
   s->view.tt_slots = s->tt_nslot;
   s->view.tt_nsub = 1 << m;
@@ -487,6 +495,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.stats_part = s->d_stats;
   v.err = s->d_err;
   v.ttab = nullptr;                       // (until the first pool load: ensure_table)
+  v.ttab4 = nullptr;
+  v.tt_blk = 0;
   v.tt_cells = s->d_ttcells;
   v.tt_nsub = 1;
   v.n_envs = n_envs;
@@ -592,6 +602,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_sync);
   (void)hipFree(s->d_sync_graph);
   (void)hipFree(s->d_ttab);
+  (void)hipFree(s->d_ttab4);
   (void)hipFree(s->d_ttcells);
   delete s;
   return CRAFT_OK;

@@ -315,6 +315,30 @@ __global__ __launch_bounds__(256) void teach_table_kernel(SimView v, TableArgs a
   if (ql == 0) const_cast<uint16_t*>(v.ttab)[(size_t)row * per_row + k] = e;
 }
 
+// The rows' answers again as the label each gives (go_leaf_action), 4 bits per (dir, cell), one
+// tt_blk-byte block per (trow, slot): what craft_rollout_teach caches per env in LDS.
+__global__ __launch_bounds__(256) void tt_nibble_kernel(SimView v, TableArgs a) {
+  const int C = v.C, S = v.tt_slots, blk = v.tt_blk;
+  const int64_t per_row = (int64_t)v.tt_nsub * S * blk;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)a.count * per_row) return;
+  const int64_t r = i / per_row, k = i - r * per_row;
+  const int64_t b = k / blk;                                          // sub * S + slot
+  const int j = (int)(k - b * blk);
+  const int64_t row = a.first + r;
+  const uint16_t* e = v.ttab + (row * v.tt_nsub * S + b) * 4 * C;
+  auto code = [&](int idx) -> uint32_t {
+    if (idx >= 4 * C) return 15u;
+    const uint32_t x = e[idx];
+    if (!(x & 0x8000u)) return 15u;                                   // not computed
+    const int fa = (int)((x >> 10) & 7u) - 1, len = (int)(x & 0x3ffu) - 1;
+    if (!(x & 0x4000u) || len == 0) return 5u;                         // the reference raises
+    if (len < 0) return 4u;                                            // no target: STOP
+    return (uint32_t)fa;
+  };
+  const_cast<uint8_t*>(v.ttab4)[(row * v.tt_nsub * S + b) * blk + j] = (uint8_t)(code(2 * j) | (code(2 * j + 1) << 4));
+}
+
 hipError_t launch_teach_table(int nw, const SimView& v, int32_t first, int32_t count, const int32_t* kinds,
                               hipStream_t st) {
   if (!v.ttab || count <= 0 || v.tt_slots <= 0) return hipSuccess;
@@ -333,6 +357,11 @@ hipError_t launch_teach_table(int nw, const SimView& v, int32_t first, int32_t c
   else if (nw <= 5) CRAFT_TT(5);
   else CRAFT_TT(8);
 #undef CRAFT_TT
+  if (v.ttab4) {
+    const int64_t bytes = (int64_t)count * v.tt_nsub * v.tt_slots * v.tt_blk;
+    if ((bytes + 255) / 256 > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(tt_nibble_kernel, dim3((unsigned)((bytes + 255) / 256)), dim3(256), 0, st, v, a);
+  }
   return hipGetLastError();
 }
 
