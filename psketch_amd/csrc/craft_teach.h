@@ -527,6 +527,10 @@ __device__ __forceinline__ uint16_t tt_encode(bool ok, int fa, int len) {
 __device__ __forceinline__ const uint16_t* tt_row(const SimView& v, int trow) {
   return v.ttab ? v.ttab + (size_t)trow * v.tt_slots * 4 * v.C : nullptr;
 }
+// The same row as 4-bit labels (SimView::ttab4), or null.
+__device__ __forceinline__ const uint8_t* tt_row4(const SimView& v, int trow) {
+  return v.ttab4 ? v.ttab4 + (size_t)trow * v.tt_slots * v.tt_blk : nullptr;
+}
 // The table row of an env of pool row `scen` that has cleared `ncl` cells this episode, cleared(c)
 // telling which: scen * tt_nsub + the subset of the row's listed clearable cells it cleared (w0,
 // w1 = tt_cells[scen]), or -1 when it cleared a cell the table does not list (or there is no
@@ -633,7 +637,8 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
                                          const uint32_t* row32, const uint32_t (&m)[8],
                                          const uint8_t* iv, const Agent& s, int task, int ql,
                                          bool want_len, int& len_out, int& err_out, bool conn,
-                                         const uint16_t* ttab = nullptr, int* defer = nullptr) {
+                                         const uint16_t* ttab = nullptr, int* defer = nullptr,
+                                         const uint8_t* t4 = nullptr) {
   const int H = v.H, C = v.C;
   auto kind_at = [&](int c) -> int {
     const uint32_t w = row32[c >> 2];
@@ -698,6 +703,18 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
       } else if (goal == CRAFT_GOAL_GO) {
         if constexpr (DEFER) {
           const int slot = ttab ? tt_slot_of(v, arg) : -1;
+          if (t4 && slot >= 0) {                                         // the label, 4 bits (ttab4)
+            const int idx = s.dir * C + s.x * H + s.y;
+            const uint32_t code = (t4[slot * v.tt_blk + (idx >> 1)] >> (4 * (idx & 1))) & 0xfu;
+            if (code == 15u) {
+              *defer = arg;                                              // not in the table: a BFS later
+              err_out = 0;
+              return kTeachDeferred;
+            }
+            if (code < 4u) action = (int)code;
+            else if (code == 4u) action = CRAFT_STOP;
+            else err = CRAFT_ETEACHER;                                   // the reference raises
+          } else {
           const uint32_t e = slot >= 0 ? ttab[(slot * 4 + s.dir) * C + s.x * H + s.y] : 0u;
           if (!(e & 0x8000u)) {
             *defer = arg;                                                // a BFS, done densely later
@@ -705,6 +722,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
             return kTeachDeferred;
           }
           action = go_leaf_action((e & 0x4000u) != 0, (int)((e >> 10) & 7u) - 1, (int)(e & 0x3ffu) - 1, err);
+          }
         } else {
           int fa = -1, len = -1;
           leaf_ok = closest(arg, fa, len, true);

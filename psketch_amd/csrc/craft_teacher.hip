@@ -77,7 +77,8 @@ __device__ __forceinline__ int teach_item(const SimView& v, const TeachArgs& a, 
   int len = -1, err = 0, defer = -1;
   const int action = teach_env<NW, LANES, DEFER>(v, s_tab, s_sub, row32, m, iv, s, task, ql, a.len_out != nullptr,
                                                  len, err, v.pool_conn[s.scen] != 0,
-                                                 trow >= 0 ? tt_row(v, trow) : nullptr, &defer);
+                                                 trow >= 0 ? tt_row(v, trow) : nullptr, &defer,
+                                                 DEFER && trow >= 0 ? tt_row4(v, trow) : nullptr);
   if (DEFER && action == kTeachDeferred) return defer;
   if (lead) {
     if (err) latch_error(v.err, err, slot);

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
         action = teach_env<NW, TL, true>(v, s_task, s_tsub, reinterpret_cast<const uint32_t*>(s_grid + e * v.GS),
                                    m0, s_inv + e * kInvStride, s, s.task, ql, false, len, err,
                                    ((ti >> 9) & 1u) != 0, (v.tt_fused && ((ti >> 10) & 1u)) ? tt_row(v, (int)(ti >> 11)) : nullptr,
-                                   &defer);
+                                   &defer, (v.tt_fused && ((ti >> 10) & 1u)) ? tt_row4(v, (int)(ti >> 11)) : nullptr);
         if (err && ql == 0) latch_error(v.err, err, i);
         if (action == kTeachDeferred && ql == 0)
           s_work[__hip_atomic_fetch_add(&s_wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
