@@ -1242,4 +1242,22 @@ int craft_set_state(craft_sim_t* s, const int32_t* slots, int64_t n, const int32
   return CRAFT_OK;
 }
 
+// Test hook, not part of include/craft.h: craft_host::hint_tables for a configuration, exactly as
+// the HIP library builds them at craft_sim_create for the teacher-labelled rollout's walk
+// (tests/test_hint_tables.py checks every leaf against the reference's find_incomplete_subtask).
+int craft_debug_hint_tables(const craft_config_t* cfg, uint32_t* desc, uint8_t* leaf, int32_t cap,
+                            int32_t* n_leaf) {
+  if (!cfg || !desc || cap < 0) return CRAFT_EINVAL;
+  std::string msg;
+  if (craft_host::validate_config(cfg, msg) != CRAFT_OK) return CRAFT_EINVAL;
+  std::vector<uint16_t> tab(CRAFT_MAX_TASKS, 0);
+  std::vector<int32_t> sub(CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS, 0);
+  craft_host::task_tables(*cfg, tab.data(), sub.data());
+  std::vector<uint8_t> lv;
+  craft_host::hint_tables(*cfg, tab.data(), sub.data(), desc, lv);
+  if (n_leaf) *n_leaf = (int32_t)lv.size();
+  if (leaf && !lv.empty()) std::memcpy(leaf, lv.data(), std::min<size_t>((size_t)cap, lv.size()));
+  return CRAFT_OK;
+}
+
 }  // extern "C"
