@@ -88,6 +88,11 @@ def parse(argv=None):
     p.add_argument("--teacher-mode", choices=("fused", "separate"), default="fused",
                    help="teacher workload: one craft_step_teach launch per tick, or craft_teacher "
                         "then craft_step")
+    p.add_argument("--teacher-actions", choices=("policy", "label", "mix"), default="policy",
+                   help="teacher workload, K-tick launches: the hashed policy (DAgger labels of a "
+                        "scripted policy's states), every env acting on its own label "
+                        "(make_data.get_reference_actions' demonstrations at scale, auto-reset), or "
+                        "behaviour cloning on a fixed half of the envs (imitation.py:56-57)")
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--world", default="craft_medium_12x12")
     p.add_argument("--pool", type=int, default=1024)
@@ -137,6 +142,8 @@ def parse(argv=None):
         p.error("--tile must be 0, 16, 32 or 64")
     if args.workload == "teacher" and args.teacher_mode == "separate":
         args.ticks_per_launch = 1                 # craft_teacher + craft_step: one tick per launch pair
+    if args.teacher_actions != "policy" and (args.workload != "teacher" or args.ticks_per_launch < 2):
+        p.error("--teacher-actions label / mix: the teacher workload's K-tick launches only")
     return args
 
 
@@ -348,6 +355,10 @@ def run(args):
     done = torch.empty((R, n), dtype=torch.uint8, device=dev)
     success = torch.empty((R, n), dtype=torch.int8, device=dev)
     labels = torch.empty((R, n), dtype=torch.int32, device=dev)
+    # --teacher-actions label / mix: the labels of the reset states, then each launch's last
+    label_in = [sim.teacher()[0].clone()] if teacher and args.teacher_actions != "policy" else [None]
+    bc_mask = (torch.as_tensor(np.random.RandomState(args.seed + env_base).binomial(1, 0.5, size=n)
+                               .astype(np.uint8), device=dev) if teacher and args.teacher_actions == "mix" else None)
 
     tick = 0
 
@@ -368,10 +379,16 @@ def run(args):
                              done=done[r], success=success[r])
                 tick += 1
         elif teacher:
-            # k ticks and every env's label per tick, one craft_rollout_teach launch
+            # k ticks and every env's label per tick, one craft_rollout_teach launch; with label
+            # actions the previous launch's last labels are this one's label_in
+            src = {}
+            if args.teacher_actions != "policy":
+                src = dict(label_in=label_in[0], label_actions=args.teacher_actions == "label",
+                           behavior_clone=bc_mask if args.teacher_actions == "mix" else None)
             sim.rollout_teach(k, seed=args.seed, tick0=tick, obs=ring, reward=reward, done=done,
-                              success=success, labels=labels)
+                              success=success, labels=labels, **src)
             tick += k
+            label_in[0] = labels[(tick - 1) % R]
         else:
             if args.obs_only:
                 sim.rollout(k, seed=args.seed, tick0=tick, obs=ring)
@@ -473,6 +490,8 @@ def run(args):
             workload += f"_obs_{sim.obs_format}"
         if teacher:
             workload += "_" + args.teacher_mode
+            if args.teacher_actions != "policy":
+                workload += "_" + ("label_actions" if args.teacher_actions == "label" else "bc_mix")
         traffic = pmc_traffic(args, workload, k_eff)
         if teacher and K > 1:
             bound = "hbm (the teacher's walk and BFS run in the interval's slack beside the stream)"
@@ -532,6 +551,9 @@ def run(args):
                                                 args.cpu_seconds)
                 except Exception as e:      # the C leg stands alone if process pools are refused
                     np_leg = {"error": f"{type(e).__name__}: {e}"}
+            if teacher and args.teacher_actions != "policy":
+                c_leg["note"] = ("the C leg acts on the hashed policy, not on the labels: the same "
+                                 "step, features and teacher work per env-step")
             line["cpu_baseline"] = dict(c_leg, **({"python_numpy": np_leg} if np_leg is not None else {}))
         print(json.dumps(line), flush=True)
     D.shutdown()
