@@ -204,7 +204,7 @@ struct RolloutArgs {       // craft_rollout: n_ticks ticks in one launch
   const int32_t* label_in; // [n_envs] the teacher's label of each slot's state before tick0
   const uint8_t* bc;       // [n_envs] behaviour cloning: the slot acts on its label, or null
   int32_t label_actions;   // 1: every slot acts on its label (make_data.get_reference_actions)
-  int32_t lsync;           // labels feed some slot's actions (label_actions or bc)
+  int32_t lsync;           // labels feed some slot's actions (label_actions or bc): 1 row sync, 2 C looks up
   int32_t use_table;       // the teacher reads the teacher table for pristine grids
   int32_t* labels;         // [ring][n_envs] the label of every slot's new state, or null
   int32_t* rec;            // [ring][n_envs] the action taken (-1: none), or null

@@ -203,7 +203,15 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
 #define RT_ACC(k, t0) ((void)(t0))
 #endif
   const bool want_obs = a.obs != nullptr;
-  const bool lsync = a.lsync != 0;                                    // labels feed some env's actions
+  // labels feed some env's actions: (1) each item's row completes inside its interval, before the
+  // tick that acts on it; (2) the transition wave looks its labels up itself (hint table, nibble
+  // table) and waits only for the row's BFS answers, the teacher's table answers keep their lag
+#if defined(RT_U16_GATHER)
+  const int lmode = a.lsync ? 1 : 0;
+#else
+  const int lmode = a.lsync == 2 && !(v.ttab && a.use_table && !v.ttab4) ? 2 : a.lsync ? 1 : 0;
+#endif
+  const bool lsync = lmode != 0;
   const int n_tiles = (int)((n + TILE - 1) / TILE);
   const uint32_t n_units = (uint32_t)n_tiles;                          // one unit per tile: all K ticks
 
@@ -254,6 +262,13 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     uint32_t clr = 0, clr_prev = 0, chg = 0;
     constexpr uint32_t kRestart = 0x80000000u;
     int sync = 0, lab0 = 0;
+    // (label actions) the label of the state the last tick made, looked up by this wave itself:
+    // a label byte, kCNib | the nibble's position in c_word (the nibble table's dword, loaded at
+    // the end of the last tick), or kCRow: the teacher's row (the walk fallback, BFS answers, errors)
+    constexpr uint32_t kCRow = 0x80000000u, kCNib = 0x40000000u;
+    uint32_t c_tag = kCRow, c_word = 0;
+    uint3 c_hd = make_uint3(0u, 0u, 0u);                               // the task's hint descriptor
+    uint2 c_cw = make_uint2(~0u, ~0u);                                 // the row's listed clearable cells
     int ncl = 0;                                                       // cells cleared this episode
     bool live = false, lsrc = false;
     int64_t slot = 0;
@@ -318,8 +333,13 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         task_word = s_task[s.task];
         conn = v.pool_conn[s.scen];
         if (v.ttab) {                                                  // the row's clearable cells the table lists
-          s_tcell[2 * lane] = v.tt_cells[2 * (size_t)s.scen];
-          s_tcell[2 * lane + 1] = v.tt_cells[2 * (size_t)s.scen + 1];
+          c_cw = make_uint2(v.tt_cells[2 * (size_t)s.scen], v.tt_cells[2 * (size_t)s.scen + 1]);
+          s_tcell[2 * lane] = c_cw.x;
+          s_tcell[2 * lane + 1] = c_cw.y;
+        }
+        if (lsync) {
+          const uint4 hd = s_hdesc[s.task];
+          c_hd = make_uint3(hd.x, hd.y, hd.z);
         }
         ncl = 0;
 #pragma unroll
@@ -364,17 +384,101 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    // ---- (label actions) the teacher's decision for this lane's new state, as the teacher wave's
+    // walk makes it (D_WALK below: hint table leaf, then the nibble table's entry), or kCRow ----
+#if defined(RT_U16_GATHER)
+    const bool c_tab = false;
+#else
+    const bool c_tab = v.ttab4 != nullptr && v.ttab != nullptr && a.use_table;
+#endif
+    auto c_label = [&](const uint8_t* gr, const uint8_t* ivb) __attribute__((always_inline)) -> uint32_t {
+      if (s.frozen) return 0xffu;                                      // -1: the label of a done env
+      const int facing = gr[(s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir))];
+      const uint4 hd = make_uint4(c_hd.x, c_hd.y, c_hd.z, 0u);
+      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(ivb);
+      uint32_t have = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) have |= byte_tops(nonzero_bytes(ivw[w])) << (4 * w);
+      // the listed cells cleared: from the episode's cleared-cell list (clr), or the grid past 3
+      uint32_t cleared = 0;
+      if (!(clr >> 31)) {
+        const uint32_t nc = (clr >> 24) & 3;
+        const uint32_t k0 = nc > 0 ? (clr & 0xffu) : 0x100u, k1 = nc > 1 ? ((clr >> 8) & 0xffu) : 0x100u,
+                       k2 = nc > 2 ? ((clr >> 16) & 0xffu) : 0x100u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t c = ((j < 4 ? c_cw.x : c_cw.y) >> (8 * (j & 3))) & 0xffu;
+          cleared |= (uint32_t)(c != 0xffu && (c == k0 || c == k1 || c == k2)) << j;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t c = ((j < 4 ? c_cw.x : c_cw.y) >> (8 * (j & 3))) & 0xffu;
+          cleared |= (uint32_t)(c != 0xffu && gr[c != 0xffu ? c : 0u] == 0) << j;
+        }
+      }
+      if (hd.z & craft_host::kHintWalk) {                              // (the host picks mode 1 for these)
+        if (lmode == 2) latch_error(v.err, CRAFT_EINVARIANT, slot);
+        return kCRow;
+      }
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < craft_host::kHintPreds; ++j) {
+        const uint32_t b = ((j < 4 ? hd.x : hd.y) >> (8 * (j & 3))) & 0xffu;
+        const uint32_t kd = b & 0x3fu;
+        const uint32_t t = (b & 0x40u) ? (uint32_t)(facing == (int)kd) : (have >> (kd & 31u)) & 1u;
+        bits |= ((b >> 7) & t) << j;
+      }
+      const uint32_t lf = s_hleaf[hd.z + bits];
+      if (lf == craft_host::kHintErr) {                                // the reference raises (as the teacher latches)
+        latch_error(v.err, CRAFT_ETEACHER, slot);
+        return 0xfeu;                                                  // -2
+      }
+      if (lf == craft_host::kHintStop) return (uint32_t)CRAFT_STOP;
+      if (lf == craft_host::kHintUse) return (uint32_t)CRAFT_USE;
+      const int trow = c_tab && ncl == __popc(cleared) ? (int)s.scen * v.tt_nsub + (int)cleared : -1;
+      const int sl = trow >= 0 ? tt_slot_of(v, (int)lf) : -1;
+      if (sl < 0) return kCRow;
+      const uint32_t idx = (uint32_t)(s.dir * C + s.x * H + s.y);
+      const uint32_t req = ((uint32_t)trow * (uint32_t)v.tt_slots + (uint32_t)sl) * (uint32_t)(v.tt_blk >> 2) + (idx >> 3);
+      c_word = reinterpret_cast<const uint32_t*>(v.ttab4)[req];       // decoded next tick
+      return kCNib | (idx & 7u);
+    };
     // ---- C: tick k (item g) into buffer k & 1 (trainers/imitation.py:43-73) ----
     auto tick_c = [&](int k, uint32_t g) __attribute__((always_inline)) {
       const int64_t tick = a.tick0 + k;
       int d = 0, succ = -1, counted = 0, act = 0;
       uint8_t* gr = grid_of(k);
       uint8_t* iv = inv_of(k);
-      // the label of this env's current state: label_in (the unit's first tick) or the teacher's
-      // row of item g - 1, once complete (the teacher finishes each item inside its interval)
-      if (k > 0 && __ballot(live && lsrc)) {
-        for (uint32_t spins = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                     &s_ctrl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < g;) {
+      // the label of this env's current state: label_in (the unit's first tick), this wave's own
+      // lookup, or the teacher's row of item g - 1 once complete (the teacher finishes each item
+      // inside its interval)
+      int clab = 0;
+      bool use_row = false;
+      if (k > 0 && live && lsrc) {
+        if (c_tag & kCNib) {
+          const uint32_t code = (c_word >> (4 * (c_tag & 7u))) & 0xfu;
+          clab = code < 4 ? (int)code : code == 4 ? CRAFT_STOP : -2;
+          if (code > 4)                                                // raises / no entry (as the teacher's decode)
+            latch_error(v.err, code == 5 ? CRAFT_ETEACHER : CRAFT_EINVARIANT, slot);
+        } else if (c_tag & kCRow) {
+          use_row = true;
+        } else {
+          clab = (int)(int8_t)(c_tag & 0xffu);
+        }
+      }
+      // mode 1: the row complete; mode 2: the row's BFS answers in (after its walk: s_ctrl[2])
+      if (k > 0 && __ballot(live && lsrc && use_row)) {
+        const uint32_t* R = s_rows + ((g - 1) & (kRtRows - 1)) * RW;
+        for (uint32_t spins = 0;;) {
+          bool ready = __builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(&s_ctrl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= g;
+          if (ready && lmode == 2) {
+            const uint32_t rc = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&R[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            ready = !(rc & kRowFill) || ((rc >> 8) & 0xffu) == 0;       // (0 / storing: complete)
+          }
+          if (ready) break;
           __builtin_amdgcn_s_sleep(1);
           if (++spins > kRtSpinCap) { latch_error(v.err, CRAFT_EINVARIANT, rt_where(1, g, 0)); break; }   // never hang
         }
@@ -416,7 +520,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           const uint64_t gid = (uint64_t)(v.env_base + slot);
           act = (int)((uint32_t)(splitmix64(a.seed ^ (gid << 20) ^ (uint64_t)tick) >> 32) % 6u);
         }
-        if (lsrc) act = k == 0 ? lab0 : (int)s_rows[((g - 1) & (kRtRows - 1)) * RW + 4 + lane];
+        if (lsrc) act = k == 0 ? lab0 : use_row ? (int)s_rows[((g - 1) & (kRtRows - 1)) * RW + 4 + lane] : clab;
         bool restart = false;
         if (s.frozen) {
           d = 1;
@@ -466,6 +570,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         st = pack_state(s);
         RT_ACC(3, tc2);
         const uint64_t tc3 = RT_CLK();
+        if (lsync && lsrc && k + 1 < a.n_ticks) c_tag = c_label(gr, iv);
         // done, success, reward and the recorded action (action_seqs, imitation.py:59-61) leave
         // from the streaming waves, one array each
         s_cout[(k & 1) * TILE + lane] = make_uint2((uint32_t)d | ((uint32_t)(succ + 1) << 1) | ((uint32_t)counted << 3) |
@@ -680,7 +785,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         uint32_t* R = s_rows + row * RW;
         R[4 + env] = (uint32_t)label;
         if (err) latch_error(v.err, err, (int64_t)R[2] * TILE + env);
-        __hip_atomic_fetch_add(&R[0], 0xffffffffu, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&R[0], 0u - 0x101u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);   // (and a BFS one)
       }
       q.ph = kQIdle;
     };
@@ -1056,7 +1161,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             // decode the item fetched kRtLag walks ago (its slot; with label actions every item is
             // decoded in its own interval), then fetch this one's
             const int q = (int)(g & (kRtLag - 1));
-            if (!lsync) decode_slot(q, false);
+            if (lmode != 1) decode_slot(q, false);
             const bool any_req = __ballot(req != ~0u) != 0;          // (the whole wave votes)
             if (lane < TILE) {
               s_treq[q * TILE + lane] = req;
@@ -1080,13 +1185,17 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           const int row = (int)((gbase + (uint32_t)i) & (kRtRows - 1));
           push_jobs(bj, w_need == 2, s_grid + (i & 1) * TILE * GS + lane * GS, (w_key >> 12) & 0xff, w_key & 0xff,
                     (w_key >> 8) & 3, (w_key >> 20) & 1, row);
-          // the row's control word last: the labels still pending (0 = complete)
-          const uint32_t pending = (uint32_t)__popcll(__ballot(w_need != 0));
+          // the row's control word last: the labels still pending (0 = complete), the BFS ones
+          // among them in bits 8-15
+          const uint32_t pending = (uint32_t)__popcll(__ballot(w_need != 0)) | ((uint32_t)__popcll(bj) << 8);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (lane == 0)
+          if (lane == 0) {
             __hip_atomic_store(&s_rows[row * RW], kRowFill | pending, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-          duty = lsync ? D_SYNC : D_BAR;
-          if (lsync) decode_slot((int)((gbase + (uint32_t)i) & (kRtLag - 1)), true);   // (after the row's count)
+            if (lmode == 2)                                            // item i walked: its BFS count is out
+              __hip_atomic_store(&s_ctrl[2], gbase + (uint32_t)i + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          duty = lmode == 1 ? D_SYNC : D_BAR;
+          if (lmode == 1) decode_slot((int)((gbase + (uint32_t)i) & (kRtLag - 1)), true);   // (after the row's count)
           break;
         }
         case D_SYNC: {                                                 // label actions: item i complete
@@ -1098,7 +1207,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           break;
         }
         case D_DRAIN:                                                  // after the last barrier: the fetches
-          if (!lsync)                                                  // and the BFS jobs left
+          if (lmode != 1)                                              // and the BFS jobs left
             for (int q = 0; q < kRtLag; ++q) decode_slot(q, true);
           if (busy()) wait = true;
           else duty = D_EXIT;

@@ -162,6 +162,7 @@ struct craft_sim {
   // rewrites the previous launch's observation buffer, as a trainer's loop does, every other
   // teacher always; 1 always; 2 never), and teacher lanes per query (0 = each kernel's default)
   int teach_table = 0;
+  bool hint_walk = false;           // some task keeps the hint walk (no hint table: craft_host.h)
   int teach_lanes = 0;
   const void* last_teach_obs = nullptr;
   int32_t tt_kinds[16] = {};        // its slots' target kinds
@@ -492,6 +493,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   v.task_sub = s->d_task_sub;
   v.hint = s->d_hint;
   v.hint_bytes = (int32_t)hint_leaf.size();
+  for (int t = 0; t < cfg->n_tasks; ++t) s->hint_walk |= (hint[4 * t + 2] & craft_host::kHintWalk) != 0;
   v.stats_part = s->d_stats;
   v.err = s->d_err;
   v.ttab = nullptr;                       // (until the first pool load: ensure_table)
@@ -936,7 +938,9 @@ int craft_rollout_teach(craft_sim_t* s, const craft_rollout_teach_args_t* x, voi
   a.label_in = x->label_in;
   a.bc = x->behavior_clone;
   a.label_actions = x->label_actions != 0;
-  a.lsync = lsync;
+  // 2: the transition wave looks labels up itself and waits only for BFS answers; 1: it waits
+  // for each item's whole row (a task without a hint table: the walk stays with the teacher)
+  a.lsync = lsync ? (s->hint_walk ? 1 : 2) : 0;
   a.use_table = s->teach_table != 2;              // auto = always: the reads overlap the stream
   a.labels = x->labels;
   a.rec = x->action_record;

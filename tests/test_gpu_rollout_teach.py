@@ -173,9 +173,11 @@ def test_demonstrations_regenerated_on_gpu(golden, split):
     assert (host(sat) == 1).all()
 
 
-def test_rollout_teach_with_and_without_table():
+@pytest.mark.parametrize("mode", ["given", "label"])
+def test_rollout_teach_with_and_without_table(mode):
     """The teacher table (pristine grids answered at pool load) against every query running the
-    BFS (craft_sim_tune_teach table = 2): identical labels."""
+    BFS (craft_sim_tune_teach table = 2): identical labels.  With label actions the transition
+    wave looks labels up itself (table) or waits for every go label's BFS answer (no table)."""
     world, W, n, T = "craft_medium_12x12", 12, 32768, 40
     cfg, pool, specs = _setup(world, W, n, seed=3)
     a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
@@ -187,7 +189,10 @@ def test_rollout_teach_with_and_without_table():
     for s in (a, b):
         s.reset(*specs)
         r = _rings(s, T)
-        s.rollout_teach(T, actions=acts, **r)
+        if mode == "label":
+            s.rollout_teach(T, label_in=s.teacher()[0].clone(), label_actions=True, **r)
+        else:
+            s.rollout_teach(T, actions=acts, **r)
         s.check()
         outs.append(r)
     for k in outs[0]:
@@ -223,10 +228,12 @@ def test_rollout_teach_graph_replay():
     b.check()
 
 
-def test_rollout_teach_hint_walk_fallback():
+@pytest.mark.parametrize("mode", ["policy", "label"])
+def test_rollout_teach_hint_walk_fallback(mode):
     """A hint tree with more satisfies() predicates than the tabulated walk takes (make[ladder]
     over bed, axe and shears: 15) keeps the walk itself; mixed with tabulated tasks in one tile,
-    labels equal craft_step_teach's (teach_env's walk) tick by tick."""
+    labels equal craft_step_teach's (teach_env's walk) tick by tick.  With label actions such a
+    config keeps the row-synchronous mode (every item's row complete before the next tick)."""
     import copy
     from psketch_amd import gamedef
     hints = copy.deepcopy(gamedef.HINTS)
@@ -244,13 +251,18 @@ def test_rollout_teach_hint_walk_fallback():
     a.reset(*specs)
     b.reset(*specs)
     out = _rings(a, T)
-    a.rollout_teach(T, seed=2, **out)
+    label = mode == "label"
+    cur = b.teacher()[0].clone()
+    a.rollout_teach(T, seed=2, label_in=cur.clone() if label else None, label_actions=label, **out)
     ob = torch.empty((n, a.n_features), dtype=torch.float32, device="cuda")
     lb = torch.empty(n, dtype=torch.int32, device="cuda")
+    src = torch.ones(n, dtype=torch.uint8, device="cuda") if label else None
     for t in range(T):
-        b.step(None, seed=2, tick=t, obs=ob, labels=lb)
+        b.step(None, seed=2, tick=t, obs=ob, labels=lb, ref_actions=cur if label else None, behavior_clone=src)
         assert torch.equal(out["labels"][t], lb), t
-    assert (host(out["labels"])[:, np.asarray(specs[4]) == ladder] >= 0).mean() > 0.5
+        cur = lb.clone()
+    if not label:
+        assert (host(out["labels"])[:, np.asarray(specs[4]) == ladder] >= 0).mean() > 0.5
     a.check()
     b.check()
 

@@ -6,7 +6,9 @@ each wave spends working and waiting at the barrier; the teacher wave's walk, de
 BFS steps and idle time.
 
   python tools/rt_stamps.py --build            # here (CPU): psketch_amd/lib/libpsketch_craft_rtst.so
-  python tools/rt_stamps.py [K ...]             # on the GPU box (config 5: 65,536 envs)"""
+  python tools/rt_stamps.py [--label] [K ...]   # on the GPU box (config 5: 65,536 envs)
+
+--label: every env acts on its label (demonstrations: label_actions, label_in the last tick's row)."""
 import ctypes
 import os
 import sys
@@ -47,14 +49,19 @@ out = dict(obs=torch.empty((R, n, F), dtype=torch.float32, device="cuda"),
            action_record=torch.empty((R, n), dtype=torch.int32, device="cuda"))
 names = ["C", "D", "E2", "E3", "E4", "E5", "E6", "T"]
 tick = 0
-for K in [int(x) for x in sys.argv[1:]] or [20]:
+label = "--label" in sys.argv
+label_in = sim.teacher()[0].clone() if label else None
+for K in [int(x) for x in sys.argv[1:] if not x.startswith("-")] or [20]:
     for rep in range(3):
         st.zero_()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-        sim.rollout_teach(K, tick0=tick, **out)
+        kw = dict(label_in=label_in, label_actions=True) if label else {}
+        sim.rollout_teach(K, tick0=tick, **kw, **out)
         ev1.record()
+        if label:
+            label_in = out["labels"][(tick + K - 1) % R].clone()
         tick += K
         torch.cuda.synchronize()
     s = st.cpu().numpy().astype(np.float64).reshape(-1, 8, 8)
@@ -73,7 +80,7 @@ for K in [int(x) for x in sys.argv[1:]] or [20]:
                   f"bfs {per[w, 5]:.3f} ({s[:, w, 7].mean() / intervals:.1f} steps) idle {per[w, 6]:.3f}")
         elif nm == "C":
             print(f"  C   barrier {per[w, 0]:.3f} work {per[w, 2]:.3f} (sync {per[w, 4]:.3f} action {per[w, 5]:.3f} "
-                  f"transition {per[w, 3]:.3f} stores {per[w, 1]:.3f})")
+                  f"transition {per[w, 3]:.3f} label lookup + stores {per[w, 1]:.3f})")
         else:
             print(f"  {nm:3s} barrier {per[w, 0]:.3f} work {per[w, 2]:.3f}" +
                   (f" teacher-wait {per[w, 1]:.3f}" if w >= 2 else ""))
