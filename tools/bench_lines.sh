@@ -1,7 +1,8 @@
 #!/bin/bash
 # Every bench line of the round on one box (no profiler attached), one JSON file each in $OUT:
 # the driver's command, 512 steps, the one-tick kernel (16-slot ring and one reused buffer),
-# config 5 (teacher-labelled K-tick launches at K = 32 and 20, and the one-tick fused kernel),
+# config 5 (teacher-labelled K-tick launches at K = 32 and 20, and the one-tick fused kernel;
+# K = 20 with every env acting on its label, and with half of them: demonstrations, DAgger's mix),
 # the closed-loop trainer, the w = 5 rollout and one-tick lines, and config 5 at w = 5.
 set -u
 REPO="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -21,6 +22,8 @@ run k1_ring1 --ticks-per-launch 1 --ring 1 --steps 200 --warmup 20
 run config5 --workload teacher --steps 200 --warmup 20
 run config5_k20 --workload teacher --ticks-per-launch 20 --steps 200 --warmup 20
 run config5_k1 --workload teacher --ticks-per-launch 1 --steps 200 --warmup 20
+run config5_label --workload teacher --ticks-per-launch 20 --teacher-actions label --steps 200 --warmup 20
+run config5_mix --workload teacher --ticks-per-launch 20 --teacher-actions mix --steps 200 --warmup 20
 run trainer --workload trainer --steps 5 --warmup 2
 run w5 --world craft_medium_12x12_w5 --steps 20 --warmup 5
 run w5_k1 --world craft_medium_12x12_w5 --ticks-per-launch 1 --steps 100 --warmup 10

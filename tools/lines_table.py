@@ -8,7 +8,8 @@ import os
 import shutil
 import sys
 
-ORDER = ["driver", "steps512", "k1", "k1_ring1", "config5", "config5_k20", "config5_k1", "trainer", "w5",
+ORDER = ["driver", "steps512", "k1", "k1_ring1", "config5", "config5_k20", "config5_k1", "config5_label",
+         "config5_mix", "trainer", "w5",
          "w5_k1", "config5_w5"]
 WHAT = {
     "driver": "driver's command (`--steps 20 --warmup 5`)",
@@ -18,6 +19,8 @@ WHAT = {
     "config5": "config 5, K-tick teacher rollout, K = 32",
     "config5_k20": "config 5, K-tick teacher rollout, K = 20",
     "config5_k1": "config 5, one `craft_step_teach` per tick",
+    "config5_label": "config 5, K = 20, every env acts on its label",
+    "config5_mix": "config 5, K = 20, half the envs act on their label",
     "trainer": "trainer closed loop (live env-steps)",
     "w5": "w = 5 rollout, 20 ticks",
     "w5_k1": "w = 5, one tick per launch",
