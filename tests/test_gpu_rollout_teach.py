@@ -376,3 +376,47 @@ def test_rollout_teach_obs_formats(fmt):
         assert torch.equal(a[k], b[k]), k
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+
+
+def test_rollout_teach_label_actions_after_many_cleared_cells():
+    """Label actions from states with more than three cells cleared this episode (the transition
+    wave's lookup then reads the grid instead of its cleared-cell list) and with fewer: 60 ticks of
+    USE-heavy given actions with an axe and bridges in hand (grabs, stone and water cleared), then
+    20 ticks acting on labels in one launch, tick by tick against craft_step_teach fed its own
+    labels (no auto-reset: cleared cells stay)."""
+    world, W, n, T0, T = "craft_medium_12x12", 12, 32768, 60, 20
+    cfg, pool, specs = _setup(world, W, n, seed=8)
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    ix = a.cookbook.index
+    inv = np.zeros((n, a.n_kinds), dtype=np.int32)
+    inv[:, ix["axe"]] = 1
+    inv[:, ix["bridge"]] = 4
+    agent = np.stack([specs[1], specs[2], specs[3]], 1)
+    acts = torch.as_tensor(np.random.RandomState(5).choice(6, size=(T0, n), p=[.125, .125, .125, .125, .5, 0])
+                           .astype(np.int32), device="cuda")
+    for s in (a, b):
+        set_states(s, specs[0], agent, inv, task=specs[4])
+        s.rollout(T0, actions=acts, autoreset=False)
+    cur = b.teacher()[0].clone()
+    st = a.get_state(fields=("grid", "spec"))
+    g, sp = host(st["grid"]), host(st["spec"])
+    cleared = ((np.asarray(pool)[sp[:, 0]] != 0) & (g == 0)).sum(1)
+    assert (cleared >= 4).sum() >= 20 and (cleared <= 3).mean() > 0.2, np.bincount(cleared)   # (~0.14 % past 3)
+    out = _rings(a, T)
+    a.rollout_teach(T, tick0=T0, label_in=cur.clone(), label_actions=True, autoreset=False, **out)
+    ob = torch.empty((n, a.n_features), dtype=torch.float32, device="cuda")
+    lb = torch.empty(n, dtype=torch.int32, device="cuda")
+    recb = torch.empty(n, dtype=torch.int32, device="cuda")
+    src = torch.ones(n, dtype=torch.uint8, device="cuda")
+    for t in range(T):
+        b.step(None, tick=T0 + t, autoreset=False, obs=ob, labels=lb, action_record=recb, ref_actions=cur,
+               behavior_clone=src)
+        assert torch.equal(out["labels"][t], lb), t
+        assert torch.equal(out["action_record"][t], recb), t
+        assert torch.equal(out["obs"][t], ob), t
+        cur = lb.clone()
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    a.check()
+    b.check()
