@@ -121,24 +121,32 @@ def test_rollout_teach_hip_equals_cpu_variant(mode):
         assert torch.equal(outs[0][k], outs[1][k]), k
 
 
-@pytest.mark.parametrize("world", ["craft_medium_12x12", "craft_medium_12x12_w5"])
-def test_rollout_teach_vs_oracle_full_size(oracle_mod, world):
+@pytest.mark.parametrize("world,mode", [("craft_medium_12x12", "policy"), ("craft_medium_12x12_w5", "policy"),
+                                        ("craft_medium_12x12", "bc")])
+def test_rollout_teach_vs_oracle_full_size(oracle_mod, world, mode):
     """Config 5's launch (65,536 envs, 40 ticks of hashed actions with auto-reset, every env
     labelled every tick), with 3x3 and 5x5 windows, against the literal oracle on 256 sampled
-    global ids, run from their initial states with their own ids."""
+    global ids, run from their initial states with their own ids; bc: half the envs act on their
+    labels (the transition wave's own lookup), the label of the first tick from the oracle."""
     from oracle import rollout_oracle
     W, n, T, base = 12, 65536, 40, 65536
     cfg, pool, specs = _setup(world, W, n, pool_n=1024, seed=0, base=base)
     sim = sim_with_pool(world, n, pool, env_id_base=base)
     sim.reset(*specs)
     out = _rings(sim, T)
-    sim.rollout_teach(20, seed=5, tick0=0, **out)
-    sim.rollout_teach(20, seed=5, tick0=20, **out)
+    kw, bc, lab = {}, None, None
+    if mode == "bc":
+        bc = (np.random.RandomState(2).rand(n) < 0.5).astype(np.uint8)
+        lab = sim.teacher()[0].clone()
+        kw = dict(behavior_clone=torch.as_tensor(bc, device="cuda"))
+    sim.rollout_teach(20, seed=5, tick0=0, label_in=lab, **kw, **out)
+    sim.rollout_teach(20, seed=5, tick0=20, label_in=None if lab is None else out["labels"][19].clone(), **kw, **out)
     sim.check()
     pick = np.sort(np.random.RandomState(1).choice(n, 256, replace=False))
     o = oracle_mod.Oracle(cfg, pool)
     envs = o.init_envs(*[np.asarray(x)[pick] for x in specs])
-    ref = rollout_oracle.teach_rollout(o, envs, base + pick, T, seed=5)
+    extra = {} if bc is None else dict(label_in=host(lab)[pick], label_src=bc[pick])
+    ref = rollout_oracle.teach_rollout(o, envs, base + pick, T, seed=5, **extra)
     for k in ("labels", "action_record", "done", "success"):
         np.testing.assert_array_equal(host(out[k])[:, pick], ref[k], err_msg=k)
     assert (ref["labels"] >= 0).mean() > 0.9
