@@ -101,7 +101,8 @@ def parse(argv=None):
     p.add_argument("--tile", type=int, default=0, help="envs per workgroup (0 = default)")
     p.add_argument("--obs-store", type=int, default=-1,
                    help="0 write-back, 1 nontemporal, 2 sc1; -1: the library default (write-through, "
-                        "sc1: the measured best for craft_rollout and for craft_step on a reused buffer)")
+                        "sc1: the measured best for craft_rollout and for craft_step on a reused buffer; "
+                        "nontemporal for craft_rollout_teach)")
     p.add_argument("--ticks-per-launch", type=int, default=32,
                    help="K > 1: craft_rollout runs up to K ticks per launch (the same work per "
                         "tick); 1: one craft_step launch per tick")
@@ -340,8 +341,11 @@ def run(args):
                    pool_capacity=args.pool)
     grids, _, _ = sample_scenarios(sim.params, sim.cookbook, 123, args.pool)
     sim.load_pool(grids)
-    obs_store = args.obs_store if args.obs_store >= 0 else 2
-    sim.tune(args.tile, 0, obs_store)
+    if args.obs_store >= 0 or args.tile:
+        obs_store = args.obs_store if args.obs_store >= 0 else 2
+        sim.tune(args.tile, 0, obs_store)
+    else:                                     # the library's defaults (include/craft.h craft_sim_tune)
+        obs_store = 1 if args.workload == "teacher" and args.ticks_per_launch > 1 else 2
     sim.set_obs_format(args.obs_format)
     sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
