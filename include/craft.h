@@ -37,7 +37,9 @@
 extern "C" {
 #endif
 
-#define CRAFT_ABI_VERSION 1
+/* 2: craft_sim_tune_teach takes (kernel, lanes, table) (was (kernel)); craft_sim_tune_host,
+ * craft_sim_sync_table and craft_abi_version added. */
+#define CRAFT_ABI_VERSION 2
 
 #define CRAFT_MAX_KINDS 32       /* len(cookbook.index) incl. reserved 0 (21 for recipes.yaml) */
 #define CRAFT_MAX_RECIPES 16     /* recipes.yaml has 9 */
@@ -127,6 +129,10 @@ typedef struct craft_sim craft_sim_t;
 
 /* ---- handle lifetime ------------------------------------------------------ */
 
+/* CRAFT_ABI_VERSION of the loaded library: a caller that binds the symbols at run time (dlsym,
+ * ctypes) checks it before calling anything whose signature changed between versions. */
+int craft_abi_version(void);
+
 /* Replaces CraftWorld.__init__ (craft.py:59-109) for a batch of `n_envs`
  * environment slots on `device`.  `env_id_base` is the global id of slot 0
  * (rank * n_envs when sharded): per-env randomness is keyed by global id so
@@ -183,11 +189,25 @@ int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t thread
  *           direction; 4*W*H u16 entries per kind per (row, subset), allocated at the first pool
  *           load for pool_capacity rows with m chosen to fit 1 GiB (12x12 craft_medium: m = 6,
  *           453 MB for 1024 rows); a loaded row's entries are built by the next launch that reads
- *           the table, on its stream), for envs whose grid it lists: 0 (default) = auto
+ *           the table, on its stream, which then waits for them (craft_sim_sync_table)), for envs
+ *           whose grid it lists: 0 (default) = auto
  *           (craft_step_teach only when its launch rewrites the previous launch's observation
  *           buffer, where the reads hit the Infinity Cache; every other teacher always),
  *           1 = always, 2 = never (every query runs the BFS). */
 int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel, int32_t lanes, int32_t table);
+
+/* Host worker threads of the CPU variant of this ABI (libpsketch_craft_cpu.so), which splits
+ * every batched call over contiguous slot ranges: 0 = the machine's hardware threads (the
+ * default), else 1..1024.  Results are identical for every setting.  The HIP library runs no
+ * host workers: it validates the argument and keeps nothing. */
+int craft_sim_tune_host(craft_sim_t* sim, int32_t threads);
+
+/* Builds, on `stream`, the teacher-table entries of the pool rows craft_pool_load has loaded since
+ * the last build, and waits for them.  Every launch that reads the table (craft_step_teach,
+ * craft_rollout_teach, craft_teacher, craft_rollout_distances) does this first, so a caller needs
+ * it only before capturing such a launch into a HIP graph right after a pool load: a launch
+ * being captured refuses (CRAFT_EINVAL) to build them.  No-op when nothing is pending. */
+int craft_sim_sync_table(craft_sim_t* sim, void* stream);
 
 /* The kernel craft_step / craft_step_ex (teach == 0) or craft_step_teach (teach != 0) will
  * launch, resolved from the knobs above: *kernel = CRAFT_KERNEL_TILE / _TICK2, *envs =

@@ -98,14 +98,15 @@ def fake_policy(W, bias):
 
 
 def teach_rollout(oracle, envs, gids, n_ticks, seed=0, tick0=0, actions=None, autoreset=True,
-                  label_in=None, label_src=None):
+                  label_in=None, label_src=None, want_obs=False):
     """craft_rollout_teach restated over the C oracle, one env at a time: each tick the action of
     env i is its current label when label_src[i] (make_data.get_reference_actions,
     make_data.py:146-152; behaviour cloning, trainers/imitation.py:56-57), else actions[k][i] or
     the hashed draw of its global id gids[i]; then the tick (oracle_batch_tick) and the
     DemonstrationTeacher of the new state (-1 for a frozen env, -2 where the reference raises).
     envs: oracle envs (modified in place).  Returns per-tick arrays [n_ticks, n]: labels,
-    action_record (-1 for an env already done), done, success."""
+    action_record (-1 for an env already done), done, success; with want_obs also obs
+    [n_ticks, n, F] (float32, features() of each env's state after the tick)."""
     import oracle as O
     n = len(envs)
     gids = np.asarray(gids, dtype=np.int64)
@@ -113,6 +114,7 @@ def teach_rollout(oracle, envs, gids, n_ticks, seed=0, tick0=0, actions=None, au
     cur = np.zeros(n, dtype=np.int32) if label_in is None else np.asarray(label_in, dtype=np.int32).copy()
     out = {k: np.zeros((n_ticks, n), dtype=dt) for k, dt in
            (("labels", np.int32), ("action_record", np.int32), ("done", np.uint8), ("success", np.int8))}
+    obs = [] if want_obs else None
     for k in range(n_ticks):
         t = tick0 + k
         a = np.empty(n, dtype=np.int32)
@@ -124,13 +126,18 @@ def teach_rollout(oracle, envs, gids, n_ticks, seed=0, tick0=0, actions=None, au
             else:
                 a[i] = O.hash_action(seed, int(gids[i]), t)
         frozen = envs["frozen"].copy()
+        rows = []
         for i in range(n):
-            rc, _, _, d, s = oracle.batch_tick(envs[i:i + 1], int(gids[i]), a[i:i + 1], seed, t, autoreset,
-                                              want_obs=False)
+            rc, ob, _, d, s = oracle.batch_tick(envs[i:i + 1], int(gids[i]), a[i:i + 1], seed, t, autoreset,
+                                               want_obs=want_obs)
             if rc:
                 raise ReferenceError_(f"step raises for env {i} at tick {t}")
             out["done"][k, i] = d[0]
             out["success"][k, i] = s[0]
+            if want_obs:
+                rows.append(np.asarray(ob, dtype=np.float32).reshape(-1))
+        if want_obs:
+            obs.append(np.stack(rows))
         out["action_record"][k] = np.where(frozen != 0, -1, a)
         for i in range(n):
             if envs["frozen"][i]:
@@ -139,4 +146,6 @@ def teach_rollout(oracle, envs, gids, n_ticks, seed=0, tick0=0, actions=None, au
                 rc, lab = oracle.teacher(envs[i:i + 1], int(envs["task"][i]))
                 cur[i] = -2 if rc else lab
         out["labels"][k] = cur
+    if want_obs:
+        out["obs"] = np.stack(obs)
     return out

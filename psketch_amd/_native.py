@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libpsketch_craft.so")
 LIB_PATH = os.environ.get("PSKETCH_CRAFT_LIB", LIB_PATH)
 CPU_LIB_PATH = os.path.join(_HERE, "lib", "libpsketch_craft_cpu.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_KINDS = 32
 MAX_RECIPES = 16
 MAX_INGREDIENTS = 4
@@ -141,6 +141,9 @@ SIGNATURES = {
     "craft_sim_set_obs_format": (_i32, [_vp, _i32]),
     "craft_sim_tune_rollout": (_i32, [_vp, _i32, _i32]),
     "craft_sim_tune_teach": (_i32, [_vp, _i32, _i32, _i32]),
+    "craft_abi_version": (_i32, []),
+    "craft_sim_tune_host": (_i32, [_vp, _i32]),
+    "craft_sim_sync_table": (_i32, [_vp, _vp]),
     "craft_sim_step_shape": (_i32, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                     ctypes.POINTER(_i32)]),
     "craft_sim_rollout_shape": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
@@ -192,6 +195,9 @@ def lib(cpu=False):
             fn = getattr(l, name)
             fn.restype = res
             fn.argtypes = args
+        if l.craft_abi_version() != ABI_VERSION:
+            raise ImportError(f"{path}: ABI version {l.craft_abi_version()}, this binding is "
+                              f"{ABI_VERSION} (include/craft.h CRAFT_ABI_VERSION); rebuild it")
         _libs[cpu] = l
     return l
 

@@ -9,7 +9,7 @@
 // state word, the restart word, 32 u8 inventory counts and a 256-bit cleared-cell mask over the
 // scenario's pool row; configuration, pool and task-table checks come from craft_host.h, so
 // both libraries accept and refuse the same inputs.  Work is split over host threads by
-// contiguous slot ranges (CRAFT_CPU_THREADS, default: the hardware's).  Results equal the HIP
+// contiguous slot ranges (craft_sim_tune_host; default: the hardware's threads).  Results equal the HIP
 // library's bit for bit (tests/test_cpu_variant.py against the oracle here, tests/test_gpu_cpu_variant.py
 // against the HIP library on the GPU box).
 //
@@ -138,6 +138,12 @@ int fail(craft_sim* s, int code, const std::string& msg) {
 void latch(craft_sim* s, int code, int64_t slot) {
   int32_t z = 0;
   if (s->err_code.compare_exchange_strong(z, code)) s->err_slot.store(slot);
+}
+
+// the machine's hardware threads (craft_sim_tune_host's default)
+int hw_threads() {
+  const int hw = (int)std::thread::hardware_concurrency();
+  return hw > 0 ? hw : 1;
 }
 
 // fn(lo, hi) over [0, n) in contiguous ranges on the handle's threads
@@ -647,9 +653,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     return CRAFT_ENOMEM;
   }
   craft_host::task_tables(*cfg, s->task_tab, s->task_sub);
-  const char* e = getenv("CRAFT_CPU_THREADS");
-  const int hw = (int)std::thread::hardware_concurrency();
-  s->threads = std::max(1, e && atoi(e) > 0 ? atoi(e) : (hw > 0 ? hw : 1));
+  s->threads = hw_threads();
   *out = s;
   return CRAFT_OK;
 }
@@ -709,6 +713,20 @@ int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel, int32_t lanes, int32_t 
   s->teach_lanes = lanes;
   s->teach_table = table;      // (this variant keeps no table: every query runs the BFS)
   return CRAFT_OK;
+}
+
+int craft_abi_version(void) { return CRAFT_ABI_VERSION; }
+
+int craft_sim_tune_host(craft_sim_t* s, int32_t threads) {
+  if (!s) return CRAFT_EINVAL;
+  if (threads < 0 || threads > 1024)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_host: threads must be 0 (the machine's) or 1..1024");
+  s->threads = threads ? threads : hw_threads();
+  return CRAFT_OK;
+}
+
+int craft_sim_sync_table(craft_sim_t* s, void* /*stream*/) {
+  return s ? CRAFT_OK : CRAFT_EINVAL;      // (this variant keeps no table)
 }
 
 int craft_sim_step_shape(const craft_sim_t* s, int32_t teach, int32_t* kernel, int32_t* envs, int32_t* lanes) {

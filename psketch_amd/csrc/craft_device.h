@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdint>
 
@@ -115,18 +116,51 @@ struct SimView {
 #define STAMP_MAX(k) do {} while (0)
 #endif
 
+// The launchers' caches are per device (a process may drive several) and thread-safe (atomics).
+constexpr int kCacheDevices = 64;
+
 // Raises a kernel's dynamic-LDS limit past the default 64 KiB (gfx950 allows 160 KiB per
-// workgroup) once per kernel and size, not per launch: a host runtime call per launch costs every
-// tick of a trainer's loop, and a launch captured into a HIP graph is replayed without this code.
+// workgroup) once per kernel, device and size, not per launch: a host runtime call per launch
+// costs every tick of a trainer's loop, and a launch captured into a HIP graph is replayed without
+// this code.
 template <auto KERNEL>
 inline hipError_t ensure_lds(size_t lds) {
-  static size_t granted = 65536;
-  if (lds <= granted) return hipSuccess;
+  static std::atomic<size_t> granted[kCacheDevices];                 // 0: the default 64 KiB
+  if (lds <= 65536) return hipSuccess;
   if (lds > 163840) return hipErrorInvalidValue;
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(KERNEL),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e == hipSuccess) granted = lds;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const bool cached = dev >= 0 && dev < kCacheDevices;
+  if (cached && lds <= granted[dev].load(std::memory_order_relaxed)) return hipSuccess;
+  e = hipFuncSetAttribute(reinterpret_cast<const void*>(KERNEL), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess && cached) {
+    size_t cur = granted[dev].load(std::memory_order_relaxed);
+    while (cur < lds && !granted[dev].compare_exchange_weak(cur, lds, std::memory_order_relaxed)) {
+    }
+  }
   return e;
+}
+
+// Workgroups of KERNEL (`threads` threads, `lds` dynamic LDS bytes) the current device holds at
+// once: occupancy per CU x CUs, cached per device and LDS size (a persistent launch's grid).
+template <auto KERNEL>
+inline int resident_workgroups(int threads, size_t lds) {
+  static std::atomic<uint64_t> cache[kCacheDevices];                 // lds << 32 | workgroups
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  const bool cached = dev >= 0 && dev < kCacheDevices;
+  if (cached) {
+    const uint64_t c = cache[dev].load(std::memory_order_relaxed);
+    if ((uint32_t)c != 0 && (c >> 32) == (uint64_t)lds) return (int)(uint32_t)c;
+  }
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERNEL, threads, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+  if (dev < 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  const int r = per_cu * cus;
+  if (cached) cache[dev].store(((uint64_t)lds << 32) | (uint32_t)r, std::memory_order_relaxed);
+  return r;
 }
 
 // envs per tile of the teacher-labelled K-tick rollout (craft_rollout_teach.h rt_tile): 32 for

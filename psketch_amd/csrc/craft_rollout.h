@@ -468,18 +468,7 @@ static hipError_t launch_rollout_one(const SimView& v, const RolloutArgs& a, siz
   }
   // persistent workgroups: what the chip holds at once (occupancy of this kernel at this LDS
   // size), spread so that every workgroup runs the same number of units (no partial last round)
-  static int resident = 0;
-  static size_t resident_lds = 0;
-  if (resident == 0 || resident_lds != lds) {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>, NT, lds) != hipSuccess ||
-        per_cu < 1)
-      per_cu = 1;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-      cus = 256;
-    resident = per_cu * cus;
-    resident_lds = lds;
-  }
+  const int resident = resident_workgroups<&rollout_kernel<WIN, TILE, NT, FMT, WPE, GIVEN>>(NT, lds);
   const int64_t units = tiles * (int64_t)((a.n_ticks + a.chunk - 1) / a.chunk);
   const int64_t rounds = (units + resident - 1) / resident;
   // every workgroup owns one stats_part row; the handle has (n_envs + 15) / 16 of them

@@ -23,7 +23,8 @@
 //     task's satisfies() predicates (craft_host.h hint_tables), three rounds of LDS loads;
 //   * a go[X] leaf on a grid the teacher table lists (the pool row minus a subset of its listed
 //     clearable cells) issues the table's answer load (LDS-DMA) and decodes it kRtLag walks later
-//     (policy actions) or right away (label actions);
+//     (policy actions; the data is in LDS by the end of its own walk, see fetch) or right away
+//     (label actions);
 //   * any other go[X] leaf becomes a BFS job: the leaf lane builds the band bitsets of its grid
 //     row while the row is still current and queues them in LDS;
 //   * between its own duties the wave runs the queued jobs, one BFS level per step on 16 quads
@@ -53,17 +54,11 @@
 namespace craft {
 
 constexpr int kRtThreads = 512;        // C, D, 5 streaming waves, the teacher
-#ifndef RT_ROWS
-#define RT_ROWS 8
-#endif
-#ifndef RT_LAG
-#define RT_LAG 4
-#endif
-constexpr int kRtRows = RT_ROWS;       // label rows in flight: item g -> row g & (kRtRows - 1)
+constexpr int kRtRows = 8;       // label rows in flight: item g -> row g & (kRtRows - 1)
 constexpr int kRtQueue = 32;           // BFS jobs waiting for a quad
 // Table answers are fetched kRtLag walks ahead of their decode: a load from the table (hundreds of
 // MB, random rows) takes longer than an interval while the store stream saturates HBM.
-constexpr int kRtLag = RT_LAG;
+constexpr int kRtLag = 4;
 static_assert(kRtRows <= 16 && (kRtRows & (kRtRows - 1)) == 0 && (kRtLag & (kRtLag - 1)) == 0 && kRtLag < kRtRows,
               "rows and lag: powers of two, a fetched item's row still held when it is decoded");
 // label row control word: 0 free; kRowFill | pending labels while the teacher fills it (== kRowFill:
@@ -73,21 +68,24 @@ constexpr uint32_t kRowFill = 1u << 30, kRowStoring = 1u << 29;
 // and the wave stops waiting, so a broken invariant can never hang the GPU.
 constexpr uint32_t kRtSpinCap = 1u << 22;
 
-// LDS carve: grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation rows [2][up16(TILE*F)] |
-// inventory rows [2][TILE][36] | agent words [2][TILE] | teacher info words [2][TILE] | the tick's
-// outputs [2][TILE][2] | task table
-// [64] u16 | subtasks [64][4] | recipe words [16][3] | control words [8] | label rows
-// [8][4 + TILE] | BFS job queue [32][2 NW + 1] | table requests [4][TILE] | table words [4][64] |
-// their rows [4] | clearable cells [TILE][2] | hint table: descriptors [64][4], leaf bytes [2048]
+// LDS carve: table words [kRtLag][64] (the LDS-DMA targets, first, so that their M0 base stays
+// below 64 KiB for every window) | grid rows [2][TILE][GS] | pristine rows [TILE][GS] | observation rows
+// [2][up16(TILE*F)] | inventory rows [2][TILE][36] | agent words [2][TILE] | teacher info words
+// [2][TILE] | the tick's outputs [2][TILE][2] | task table [64] u16 | subtasks [64][4] | recipe
+// words [16][3] | control words [8] | label rows [8][4 + TILE] | BFS job queue [32][2 NW + 1] |
+// table requests [4][TILE] | their rows [4] | clearable cells [TILE][2] | hint table:
+// descriptors [64][4], leaf bytes [2048] | nibble positions [4][TILE]
 struct RtLds {
-  int pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint, tnib,
-      bytes;
+  int grid, pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint,
+      tnib, bytes;
 };
 __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
   RtLds l;
-  l.pristine = 2 * tile * GS;
-  l.obs = up16(3 * tile * GS);
+  l.tval = 0;                                              // [kRtLag][64] the words fetched (LDS-DMA)
+  l.grid = kRtLag * 64 * 4;
+  l.pristine = l.grid + 2 * tile * GS;
+  l.obs = up16(l.grid + 3 * tile * GS);
   l.inv = l.obs + 2 * up16(tile * F);
   l.agent = up16(l.inv + 2 * tile * kInvStride);
   l.tinfo = l.agent + 2 * tile * 4;
@@ -99,8 +97,7 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.rows = up16(l.ctrl + 32);
   l.jobs = up16(l.rows + kRtRows * (4 + tile) * 4);
   l.treq = up16(l.jobs + kRtQueue * (2 * NW + 1) * 4);   // [kRtLag][tile] table-entry requests
-  l.tval = l.treq + kRtLag * tile * 4;                     // [kRtLag][64] the words fetched (LDS-DMA)
-  l.tpend = l.tval + kRtLag * 64 * 4;                      // [kRtLag] their label rows (~0: none)
+  l.tpend = l.treq + kRtLag * tile * 4;                    // [kRtLag] their label rows (~0: none)
   l.tcell = l.tpend + kRtLag * 4;                          // [tile][2] each env's listed clearable cells
   l.hint = up16(l.tcell + tile * 8);                       // craft_host.h hint_tables
   l.tnib = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;   // [kRtLag][tile] nibble in the word
@@ -155,7 +152,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   const RtLds lay = rt_lds(TILE, GS, F, NW);
   // the recipe words in a VGPR (lane w: word w), loaded while every lane is active (v_readlane)
   const uint32_t rcv = v.rcw[min((int)(threadIdx.x & 63), CRAFT_MAX_RECIPES * 3 - 1)];
-  uint8_t* s_grid = smem;                                             // [2][TILE][GS] by item parity
+  uint8_t* s_grid = smem + lay.grid;                                  // [2][TILE][GS] by item parity
   uint8_t* s_pristine = smem + lay.pristine;                          // [TILE][GS]
   const int obs_buf = up16(TILE * F);
   uint8_t* s_obs = smem + lay.obs;                                    // [2][obs_buf]
@@ -206,11 +203,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   // labels feed some env's actions: (1) each item's row completes inside its interval, before the
   // tick that acts on it; (2) the transition wave looks its labels up itself (hint table, nibble
   // table) and waits only for the row's BFS answers, the teacher's table answers keep their lag
-#if defined(RT_U16_GATHER)
-  const int lmode = a.lsync ? 1 : 0;
-#else
   const int lmode = a.lsync == 2 && !(v.ttab && a.use_table && !v.ttab4) ? 2 : a.lsync ? 1 : 0;
-#endif
   const bool lsync = lmode != 0;
   const int n_tiles = (int)((n + TILE - 1) / TILE);
   const uint32_t n_units = (uint32_t)n_tiles;                          // one unit per tile: all K ticks
@@ -386,11 +379,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     };
     // ---- (label actions) the teacher's decision for this lane's new state, as the teacher wave's
     // walk makes it (D_WALK below: hint table leaf, then the nibble table's entry), or kCRow ----
-#if defined(RT_U16_GATHER)
-    const bool c_tab = false;
-#else
     const bool c_tab = v.ttab4 != nullptr && v.ttab != nullptr && a.use_table;
-#endif
     auto c_label = [&](const uint8_t* gr, const uint8_t* ivb) __attribute__((always_inline)) -> uint32_t {
       if (s.frozen) return 0xffu;                                      // -1: the label of a done env
       const int facing = gr[(s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir))];
@@ -874,9 +863,6 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       jhead += taken;
     };
     auto step = [&]() __attribute__((always_inline)) {
-#ifdef RT_NO_STEP
-      return;
-#endif
       take_jobs();
       if (q.ph == kQFwd) {
         const Bits<NW> nxt = bandn(bor(band(bshift_var(q.U, dla), q.fr), band(q.U, blocked())), q.V);
@@ -934,38 +920,32 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     auto busy = [&]() __attribute__((always_inline)) -> bool {
       return jtail != jhead || __ballot(q.ph != kQIdle) != 0;
     };
-    // Policy actions: each walk fetches its items' table words with one LDS-DMA (global_load_lds,
-    // written by inline asm so that the compiler neither waits for it nor for the LDS it fills),
-    // a dummy one when the item asks for none, so that the fetch of the item kRtLag walks back is
-    // exactly the one vmcnt(kRtLag - 1) leaves waiting for (loads complete in order; any other
-    // VMEM op of this wave, a latched error, only makes the wait stricter).
+    // Policy actions: each walk fetches its items' table words with one LDS-DMA
+    // (__builtin_amdgcn_global_load_lds: the compiler sets M0 itself), a dummy one when the item
+    // asks for none, so that the fetch of the item kRtLag walks back is exactly the one
+    // vmcnt(kRtLag - 1) leaves waiting for (loads complete in order; any other VMEM op of this
+    // wave, a latched error, only makes the wait stricter).  hipcc cannot tell the DMA's target
+    // from the rest of the dynamic LDS, so it also waits vmcnt(0) before the wave's next LDS
+    // access: the fetch lands within its walk's interval instead of kRtLag walks later.  Measured
+    // against round 5's inline asm (which set M0 by hand): 398-400 against 391-392 us per 20-tick
+    // launch, 471 against 466-475 with label actions (profiles/r06/ab_dma).
     // (the answers as 4-bit labels, SimView::ttab4: a quarter of the u16 table's footprint, so
     // more of the lines the gather touches are L2 hits; req is then the dword index)
-#ifdef RT_U16_GATHER
-    const bool nib = false;
-#else
     const bool nib = v.ttab4 != nullptr;
-#endif
     const uint32_t* tbase = reinterpret_cast<const uint32_t*>(
         nib ? (const void*)v.ttab4 : v.ttab ? (const void*)v.ttab : (const void*)v.task_tab);
     auto fetch = [&](int q, uint32_t req) __attribute__((always_inline)) {
       const uint32_t* gp = tbase + (req == ~0u ? 0u : nib ? req : req >> 1);
-      const uint32_t lds = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(s_tval + q * 64));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // the slot's last reads are done
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(lds), "v"(gp));
+      __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(s_tval + q * 64), 4, 0, 0);
     };
     // decode slot q's words (fetched kRtLag walks ago, or at the end: wait_all) into their label row
     auto decode_slot = [&](int q, bool wait_all) __attribute__((always_inline)) {
       const uint64_t tq = RT_CLK();
       const uint32_t prow = __builtin_amdgcn_readfirstlane(s_tpend[q]);
       if (prow == ~0u) { RT_ACC(3, tq); return; }
-#if defined(RT_ABL) && (RT_ABL & 8)                                   // ablation (timing only): no wait
-      if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
       if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kRtLag - 1) : "memory");
-#endif
       uint32_t* R = s_rows + prow * RW;
       const uint32_t req = lane < TILE ? s_treq[q * TILE + lane] : ~0u;
       if (req != ~0u) {
@@ -1027,7 +1007,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     auto next_in_tick = [&]() __attribute__((always_inline)) -> int {   // after the barrier opening interval i
       return i < nq ? D_WALK : D_BAR;
     };
-    uint32_t steps_run = 0;                                            // BFS levels this launch
+    uint32_t steps_run = 0;                                            // BFS levels in the current wait
     for (uint32_t idle_spins = 0;;) {
       bool wait = false;
       const uint64_t tt = RT_CLK();
@@ -1069,11 +1049,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           w_need = 0;                                                  // 1: a table answer, 2: a BFS job
           uint32_t req = ~0u;                                          // (policy actions) the ttab index asked
           uint32_t w_nib = 0;                                          // (nibble table) the nibble in that word
-#if defined(RT_ABL) && (RT_ABL & 1)                                   // ablation builds only: no walk
-          if (false) {
-#else
           if (lane < nE) {
-#endif
             // the walk's loads in three rounds, each issued together: the agent and task words and
             // the row's listed clearable cells; the facing cell, the hint descriptor, the inventory
             // and the listed cells' kinds now; the hint leaf
@@ -1130,12 +1106,6 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
                                      ? (int)(ti >> 10) * v.tt_nsub + (int)cleared : -1;
                 const int sl = trow >= 0 ? tt_slot_of(v, kind) : -1;
                 w_need = sl >= 0 ? 1 : 2;
-#if defined(RT_ABL) && (RT_ABL & 2)                                   // ablation: no table loads
-                if (w_need == 1) { w_need = 0; w_label = CRAFT_STOP; }
-#endif
-#if defined(RT_ABL) && (RT_ABL & 4)                                   // ablation: no BFS jobs
-                if (w_need == 2) { w_need = 0; w_label = CRAFT_STOP; }
-#endif
                 if (w_need == 1) {
                   if (nib) {                                           // the dword holding the nibble
                     const uint32_t idx = (uint32_t)(dir * C + x * H + y);
@@ -1145,9 +1115,6 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
                     req = (uint32_t)(((size_t)trow * v.tt_slots + sl) * 4 + dir) * C + x * H + y;
                   }
                 }
-#if defined(RT_ABL) && (RT_ABL & 16)                                  // ablation: fetch, never decode
-                if (w_need == 1) { w_need = 0; w_label = CRAFT_STOP; }
-#endif
               }
             }
           }
@@ -1167,11 +1134,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
               s_treq[q * TILE + lane] = req;
               s_tnib[q * TILE + lane] = (uint8_t)w_nib;
             }
-#if defined(RT_ABL) && (RT_ABL & 16)
-            if (lane == 0) s_tpend[q] = ~0u;
-#else
             if (lane == 0) s_tpend[q] = any_req ? (uint32_t)row : ~0u;
-#endif
             const uint64_t tf = RT_CLK();
             fetch(q, req);
             RT_ACC(1, tf);
@@ -1215,6 +1178,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         default:
           break;
       }
+      if (!wait) {                                                     // progress: the bounds below are per wait
+        idle_spins = 0;
+        steps_run = 0;
+      }
       if (!wait && duty0 == D_WALK) RT_ACC(2, tt);
       if (!wait && duty0 == D_WALK_JOBS) RT_ACC(4, tt);
       if (duty == D_EXIT) {
@@ -1231,7 +1198,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           if (lane == 0) __hip_atomic_fetch_add(&stt[7], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
           idle_spins = 0;
-          if (++steps_run > (1u << 22)) {                              // never hang the GPU (~2 s)
+          if (++steps_run > kRtSpinCap) {                              // never hang the GPU (~2 s)
             latch_error(v.err, CRAFT_EINVARIANT, rt_where(5, gbase + (uint32_t)i, (uint32_t)duty));
             break;
           }

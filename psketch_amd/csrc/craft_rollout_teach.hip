@@ -23,18 +23,7 @@ static hipError_t launch_rt_one(const SimView& v, const RolloutArgs& a, hipStrea
   }
   // persistent workgroups: what the chip holds at once, spread so that every workgroup runs the
   // same number of tiles
-  static int resident = 0;
-  static size_t resident_lds = 0;
-  if (resident == 0 || resident_lds != lds) {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kRtThreads, lds) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-      cus = 256;
-    resident = per_cu * cus;
-    resident_lds = lds;
-  }
+  const int resident = resident_workgroups<&rollout_teach_kernel<WIN, TILE, NW>>(kRtThreads, lds);
   const int64_t rounds = (tiles + resident - 1) / resident;
   const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;   // stats_part rows
   const int64_t grid = std::min<int64_t>((tiles + rounds - 1) / rounds, rows);
@@ -53,17 +42,11 @@ static hipError_t launch_rt_win(int nw, const SimView& v, const RolloutArgs& a, 
 }
 
 hipError_t launch_rollout_teach(int win, int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
-#ifdef CRAFT_RT_ONE       // diagnostic builds: the 3x3, 12x12 instantiation only (compile time)
-  (void)win;
-  (void)nw;
-  return launch_rt_one<3, 4>(v, a, st);
-#else
   switch (win) {
     case 3: return launch_rt_win<3>(nw, v, a, st);
     case 5: return launch_rt_win<5>(nw, v, a, st);
     default: return launch_rt_win<7>(nw, v, a, st);
   }
-#endif
 }
 
 }  // namespace craft

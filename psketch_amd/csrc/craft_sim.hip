@@ -283,17 +283,32 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
 }
 
 // Builds the teacher-table entries (and listed clearable cells) of the rows loaded since the last
-// build, on `stream`, ahead of the launch about to read them.
-hipError_t flush_table(craft_sim* s, void* stream) {
-  if (s->tt_dirty.empty()) return hipSuccess;
-  if (s->d_ttab)
+// build, ahead of the launch (`what`) about to read them: on that launch's stream, then a host
+// wait, so that a reader on any other stream finds the rows finished too (one wait per batch of
+// pool loads, not per launch).  Refused while the stream is being captured into a HIP graph: the
+// build would be captured with the launch (rebuilt on every replay, or never run if the capture
+// is dropped), so the caller runs one eager launch (or craft_sim_sync_table) first.  Until built,
+// a row's entries read as "not computed" (ensure_table's fill), which latches CRAFT_EINVARIANT
+// instead of a wrong label.
+int flush_table(craft_sim* s, void* stream, const char* what) {
+  if (s->tt_dirty.empty()) return CRAFT_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (s->d_ttab) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIP_TRY(s, hipStreamIsCapturing(st, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+      return fail(s, CRAFT_EINVAL, std::string(what) +
+                                       ": pool rows loaded since the last eager teacher launch have no teacher-table "
+                                       "entries yet; run craft_sim_sync_table (or one eager launch) before capturing");
     for (const auto& r : s->tt_dirty) {
       const hipError_t e = craft::launch_teach_table(craft::teach_words(s->view.W, s->view.H), s->view, r.first,
-                                                     r.second, s->tt_kinds, reinterpret_cast<hipStream_t>(stream));
-      if (e != hipSuccess) return e;
+                                                     r.second, s->tt_kinds, st);
+      if (e != hipSuccess) return hip_fail(s, e, "teacher table build");
     }
+    HIP_TRY(s, hipStreamSynchronize(st));
+  }
   s->tt_dirty.clear();
-  return hipSuccess;
+  return CRAFT_OK;
 }
 
 // The view a teacher launch gets: the table hidden when craft_sim_tune_teach says never.
@@ -348,6 +363,16 @@ void ensure_table(craft_sim* s, int max_clearable) {
     (void)hipGetLastError();
     (void)hipFree(s->d_ttab);
     s->d_ttab = nullptr;                  // no table: every query runs the BFS (same results)
+    s->d_ttab4 = nullptr;
+    return;
+  }
+  // every entry "not computed" until its row is built (flush_table): u16 0 and nibble 15 latch
+  // CRAFT_EINVARIANT in every reader instead of decoding as a label
+  if (hipMemset(s->d_ttab, 0, bytes(m)) != hipSuccess || hipMemset(s->d_ttab4, 0xff, bytes4(m)) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(s->d_ttab);
+    (void)hipFree(s->d_ttab4);
+    s->d_ttab = nullptr;
     s->d_ttab4 = nullptr;
     return;
   }
@@ -557,6 +582,21 @@ int craft_sim_tune_teach(craft_sim_t* s, int32_t kernel, int32_t lanes, int32_t 
   s->teach_lanes = lanes;
   s->teach_table = table;
   return CRAFT_OK;
+}
+
+int craft_abi_version(void) { return CRAFT_ABI_VERSION; }
+
+int craft_sim_tune_host(craft_sim_t* s, int32_t threads) {
+  if (!s) return CRAFT_EINVAL;
+  if (threads < 0 || threads > 1024)
+    return fail(s, CRAFT_EINVAL, "craft_sim_tune_host: threads must be 0 (the machine's) or 1..1024");
+  return CRAFT_OK;                          // (no host workers in this library)
+}
+
+int craft_sim_sync_table(craft_sim_t* s, void* stream) {
+  if (!s) return CRAFT_EINVAL;
+  HIP_TRY(s, hipSetDevice(s->device));
+  return flush_table(s, stream, "craft_sim_sync_table");
 }
 
 int craft_sim_step_shape(const craft_sim_t* s, int32_t teach, int32_t* kernel, int32_t* envs, int32_t* lanes) {
@@ -816,7 +856,10 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   // loop: ring 1, -2.5 us per tick) and go to HBM beside the store stream when every launch
   // writes a fresh buffer (a 16-slot ring: +0.5 us), so auto mode reads them only in the first
   // case (profiles/r04/ab5).
-  HIP_TRY(s, flush_table(s, stream));
+  {
+    const int frc = flush_table(s, stream, "craft_step_teach");
+    if (frc != CRAFT_OK) return frc;
+  }
   SimView v = teach_view(s);
   v.tt_fused = s->teach_table == 1 || (s->teach_table == 0 && (a.obs == nullptr || a.obs == s->last_teach_obs));
   s->last_teach_obs = a.obs;
@@ -946,6 +989,10 @@ int craft_rollout_teach(craft_sim_t* s, const craft_rollout_teach_args_t* x, voi
   a.use_table = s->teach_table != 2;              // auto = always: the reads overlap the stream
   a.labels = x->labels;
   a.rec = x->action_record;
+  {
+    const int frc = flush_table(s, stream, "craft_rollout_teach");
+    if (frc != CRAFT_OK) return frc;
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // the work-unit counter as craft_rollout's split kernel uses it (queue[1], one claim past the
   // last unit per workgroup); a captured launch gets the graph's own zeroed counter
@@ -971,7 +1018,6 @@ int craft_rollout_teach(craft_sim_t* s, const craft_rollout_teach_args_t* x, voi
   }
   int64_t grid = 0;
   a.grid_out = &grid;
-  HIP_TRY(s, flush_table(s, stream));
   SimView v = teach_view(s);
   // nontemporal observation stores unless tuned: they keep the table's gathered lines in L2
   // (65,536 envs, 20 ticks: 417 -> 388 us with hashed actions, 539 -> 467 us with label actions)
@@ -1035,7 +1081,10 @@ int craft_rollout_distances(craft_sim_t* s, const int32_t* tasks, const int8_t* 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   HIP_TRY(s, hipMemsetAsync(flags_out, 0, 2 * sizeof(int32_t), st));
   if (s->n_envs == 0) return CRAFT_OK;
-  HIP_TRY(s, flush_table(s, stream));
+  {
+    const int frc = flush_table(s, stream, "craft_rollout_distances");
+    if (frc != CRAFT_OK) return frc;
+  }
   hipError_t e = craft::launch_distances(craft::teach_words(s->view.W, s->view.H), teach_view(s), tasks, success, action_seqs, ticks,
                                          s->n_envs, distances_out, is_get_out, n_actions_out, flags_out, st);
   if (e != hipSuccess) return hip_fail(s, e, "craft_rollout_distances launch");
@@ -1051,7 +1100,10 @@ int craft_teacher(craft_sim_t* s, const int32_t* slots, int64_t n, const int32_t
   if (4 * s->view.C > 1000)
     return fail(s, CRAFT_EINVAL, "craft_teacher: 4*W*H > 1000 overflows the reference's BFS queue (teachers/base.py:42)");
   if (n == 0) return CRAFT_OK;
-  HIP_TRY(s, flush_table(s, stream));
+  {
+    const int frc = flush_table(s, stream, "craft_teacher");
+    if (frc != CRAFT_OK) return frc;
+  }
   hipError_t e = craft::launch_teacher(craft::teach_words(s->view.W, s->view.H), s->teach_lanes, teach_view(s), slots, tasks, n, action_out,
                                        path_len_out, reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(s, e, "craft_teacher launch");

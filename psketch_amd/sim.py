@@ -108,6 +108,17 @@ class CraftSim:
         self._check(self._L.craft_sim_tune_teach(self._h, int(kernel), int(lanes), int(table)),
                     "craft_sim_tune_teach")
 
+    def tune_host(self, threads=0):
+        """Host worker threads of the CPU variant (craft_sim_tune_host: 0 = the machine's);
+        validated and ignored by the HIP library. Results are identical for every setting."""
+        self._check(self._L.craft_sim_tune_host(self._h, int(threads)), "craft_sim_tune_host")
+
+    def sync_table(self):
+        """Build the teacher-table rows of pools loaded since the last teacher launch, on the
+        current stream, and wait (craft_sim_sync_table): needed only before capturing a teacher
+        launch into a graph right after load_pool (the capture refuses to build them)."""
+        self._check(self._L.craft_sim_sync_table(self._h, self._stream()), "craft_sim_sync_table")
+
     def step_shape(self, teach=False):
         """(kernel name, envs per tile / workgroup, teacher lanes per env) that step()
         launches, without (teach=False) or with labels= (craft_sim_step_shape)."""

@@ -237,3 +237,33 @@ def test_cpu_errors_mirror_the_hip_library():
     with pytest.raises(N.CraftError) as e:
         sim.load_pool(np.repeat(pool, 2, axis=0))
     assert e.value.status == N.ERANGE
+
+
+def test_host_threads_knob_and_abi_version_cpu():
+    """craft_sim_tune_host sets the CPU variant's worker threads (results identical for 1, 3 and
+    the machine's); out-of-range values are refused in both libraries' way; both libraries report
+    the binding's CRAFT_ABI_VERSION."""
+    assert N.lib(cpu=True).craft_abi_version() == N.ABI_VERSION == 2
+    world = "craft_medium_12x12"
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 32)
+    n = 5000
+    specs = synthetic_specs(pool, 12, 12, n, 0, seed=4, task_ids=[t.id for t in tm.dataset_tasks()])
+    outs = []
+    for threads in (1, 3, 0):
+        s = cpu_sim(world, n, pool)
+        s.tune_host(threads)
+        s.reset(*specs)
+        ring = torch.zeros((4, n, s.n_features))
+        labels = torch.zeros((4, n), dtype=torch.int32)
+        s.rollout_teach(4, seed=2, obs=ring, labels=labels)
+        s.check()
+        outs.append((ring, labels, s.stats()))
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
+    with pytest.raises(N.CraftError):
+        s.tune_host(-1)
+    with pytest.raises(N.CraftError):
+        s.tune_host(4096)
+    s.sync_table()                                   # (no table in this variant: a no-op)

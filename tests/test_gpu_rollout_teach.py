@@ -92,10 +92,8 @@ def test_rollout_teach_equals_step_teach(world, W, n, T, K, ring, mode, autorese
     b.check()
 
 
-@pytest.mark.parametrize("mode", ["policy", "bc", "label"])
-def test_rollout_teach_hip_equals_cpu_variant(mode):
-    world, W, n, T = "craft_medium_12x12", 12, 2048, 35
-    cfg, pool, specs = _setup(world, W, n, seed=2)
+def _hip_vs_cpu(world, W, n, T, mode, seed=2, pool_n=256):
+    cfg, pool, specs = _setup(world, W, n, seed=seed, pool_n=pool_n)
     g = sim_with_pool(world, n, pool)
     c = CraftSim(world, n_envs=n, device="cpu", pool_capacity=len(pool))
     c.load_pool(pool)
@@ -119,15 +117,97 @@ def test_rollout_teach_hip_equals_cpu_variant(mode):
         outs.append({k: v.cpu() for k, v in r.items()})
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+    return outs[0]
+
+
+@pytest.mark.parametrize("mode", ["policy", "bc", "label"])
+def test_rollout_teach_hip_equals_cpu_variant(mode):
+    _hip_vs_cpu("craft_medium_12x12", 12, 2048, 35, mode)
+
+
+def _world(W, win, prims=2):
+    return dict(WIDTH=W, HEIGHT=W, WINDOW_WIDTH=win, WINDOW_HEIGHT=win, N_WORKSHOPS=3, N_PRIMITIVES=prims,
+                N_WORLDS=100)
+
+
+# The instantiations no BASELINE config runs: 7x7 windows (rollout_teach_kernel<7, 16, 4>, whose LDS
+# carve passes 64 KiB: the table words' LDS-DMA target stays first in it) and 15x15 grids (8 BFS
+# words: <3, 32, 8> and <7, 16, 8>, the variants with scratch spills)
+@pytest.mark.parametrize("W,win,prims,mode", [(12, 7, 2, "policy"), (12, 7, 2, "label"), (15, 3, 4, "policy"),
+                                              (15, 7, 4, "bc")])
+def test_rollout_teach_wide_instantiations_equal_cpu_variant(W, win, prims, mode):
+    out = _hip_vs_cpu(_world(W, win, prims), W, 1024, 30, mode, pool_n=128)
+    if mode == "label":                                        # demonstrations: actions, then -1 once ended
+        assert bool((out["labels"] >= -1).all()) and bool((out["labels"][0] >= 0).all())
+    else:
+        assert (out["labels"] >= 0).float().mean() > 0.5       # labels are mostly actions, not -1/-2
+
+
+def test_rollout_teach_long_launch():
+    """A 1200-tick launch (the teacher wave's bounded waits count per wait, not per launch: no
+    error latches however long the launch) equals the same ticks in 4 launches."""
+    world, W, n, T = "craft_medium_12x12", 12, 1024, 1200
+    cfg, pool, specs = _setup(world, W, n, seed=3)
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.reset(*specs)
+    b.reset(*specs)
+    ra, rb = _rings(a, 8), _rings(b, 8)
+    a.rollout_teach(T, seed=7, **ra)
+    a.check()
+    for t0 in range(0, T, 300):
+        b.rollout_teach(300, seed=7, tick0=t0, **rb)
+    b.check()
+    for k in ra:
+        assert torch.equal(ra[k], rb[k]), k
+    np.testing.assert_array_equal(host(a.stats()), host(b.stats()))
+
+
+def test_rollout_teach_capture_right_after_pool_load():
+    """A launch captured into a graph straight after load_pool: the capture refuses to build the
+    new rows' teacher-table entries (they would be rebuilt on every replay); after sync_table the
+    captured launch replays equal to an eager one."""
+    from psketch_amd._native import CraftError
+    world, W, n, T = "craft_medium_12x12", 12, 4096, 10
+    cfg, pool, specs = _setup(world, W, n, seed=5)
+    a = sim_with_pool(world, n, pool)
+    a.reset(*specs)
+    ra = _rings(a, T)
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(CraftError, match="sync_table"):
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                a.rollout_teach(T, seed=1, **ra)
+    torch.cuda.synchronize()
+    b = sim_with_pool(world, n, pool)
+    b.reset(*specs)
+    b.sync_table()
+    rb = _rings(b, T)
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g2, stream=s):
+            b.rollout_teach(T, seed=1, **rb)
+    g2.replay()
+    torch.cuda.synchronize()
+    b.check()
+    c = sim_with_pool(world, n, pool)
+    c.reset(*specs)
+    rc = _rings(c, T)
+    c.rollout_teach(T, seed=1, **rc)
+    c.check()
+    for k in rb:
+        assert torch.equal(rb[k], rc[k]), k
 
 
 @pytest.mark.parametrize("world,mode", [("craft_medium_12x12", "policy"), ("craft_medium_12x12_w5", "policy"),
-                                        ("craft_medium_12x12", "bc")])
+                                        ("craft_medium_12x12", "bc"), ("craft_medium_12x12", "label")])
 def test_rollout_teach_vs_oracle_full_size(oracle_mod, world, mode):
     """Config 5's launch (65,536 envs, 40 ticks of hashed actions with auto-reset, every env
     labelled every tick), with 3x3 and 5x5 windows, against the literal oracle on 256 sampled
-    global ids, run from their initial states with their own ids; bc: half the envs act on their
-    labels (the transition wave's own lookup), the label of the first tick from the oracle."""
+    global ids, run from their initial states with their own ids: labels, actions, done, success
+    and every tick's observation rows; bc: half the envs act on their labels (the transition
+    wave's own lookup), the label of the first tick from the oracle; label: every env does
+    (make_data's demonstrations, auto-reset after each episode)."""
     from oracle import rollout_oracle
     W, n, T, base = 12, 65536, 40, 65536
     cfg, pool, specs = _setup(world, W, n, pool_n=1024, seed=0, base=base)
@@ -137,8 +217,12 @@ def test_rollout_teach_vs_oracle_full_size(oracle_mod, world, mode):
     kw, bc, lab = {}, None, None
     if mode == "bc":
         bc = (np.random.RandomState(2).rand(n) < 0.5).astype(np.uint8)
-        lab = sim.teacher()[0].clone()
         kw = dict(behavior_clone=torch.as_tensor(bc, device="cuda"))
+    elif mode == "label":
+        bc = np.ones(n, dtype=np.uint8)
+        kw = dict(label_actions=True)
+    if bc is not None:
+        lab = sim.teacher()[0].clone()
     sim.rollout_teach(20, seed=5, tick0=0, label_in=lab, **kw, **out)
     sim.rollout_teach(20, seed=5, tick0=20, label_in=None if lab is None else out["labels"][19].clone(), **kw, **out)
     sim.check()
@@ -146,9 +230,12 @@ def test_rollout_teach_vs_oracle_full_size(oracle_mod, world, mode):
     o = oracle_mod.Oracle(cfg, pool)
     envs = o.init_envs(*[np.asarray(x)[pick] for x in specs])
     extra = {} if bc is None else dict(label_in=host(lab)[pick], label_src=bc[pick])
-    ref = rollout_oracle.teach_rollout(o, envs, base + pick, T, seed=5, **extra)
+    ref = rollout_oracle.teach_rollout(o, envs, base + pick, T, seed=5, want_obs=True, **extra)
     for k in ("labels", "action_record", "done", "success"):
         np.testing.assert_array_equal(host(out[k])[:, pick], ref[k], err_msg=k)
+    ob = out["obs"][:, torch.as_tensor(pick, device="cuda")].cpu().numpy()
+    for t in range(T):
+        np.testing.assert_array_equal(ob[t], ref["obs"][t], err_msg=f"observations, tick {t}")
     assert (ref["labels"] >= 0).mean() > 0.9
 
 

@@ -21,7 +21,7 @@ if "--build" in sys.argv:
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import diag_build
     extra = [a for a in sys.argv[1:] if a.startswith("-D")]
-    diag_build.build(("craft_sim", "craft_rollout_teach"), ["-DCRAFT_RT_ONE"] + extra, LIB, True)
+    diag_build.build(("craft_sim", "craft_rollout_teach"), list(extra), LIB, True)
     sys.exit(0)
 
 import numpy as np  # noqa: E402
