@@ -85,6 +85,10 @@ def parse(argv=None):
                    help="trainer workload: ticks per captured HIP graph in do_rollout (0 = the "
                         "eager lookahead loop: 2.9-3.2 ms per 40-tick rollout against 2.80-2.91 "
                         "with graphs of 8 ticks, whose loop does not depend on the host's speed)")
+    p.add_argument("--trainer-teacher", choices=("fused", "side"), default="fused",
+                   help="trainer workload: the teacher fused into the tick (craft_step_teach labels "
+                        "the next tick's ref_actions) or forked beside the student's act() on a side "
+                        "stream inside the captured graphs (craft_teacher, then craft_step_ex)")
     p.add_argument("--teacher-mode", choices=("fused", "separate"), default="fused",
                    help="teacher workload: one craft_step_teach launch per tick, or craft_teacher "
                         "then craft_step")
@@ -281,6 +285,17 @@ def pmc_traffic(args, workload, k):
         if e.get("workload") == workload and e.get("ticks_per_launch", 1) == k:
             return e.get("hbm_bytes_per_launch")
     return None
+
+
+def hbm_rate(traffic, kernel_us):
+    """The real HBM rate beside the algorithmic one: the PMC bytes per launch (FETCH_SIZE +
+    WRITE_SIZE, corrected) over the kernel's launch time, and its fraction of the 8 TB/s peak.
+    Differs from `achieved` where algorithmic bytes never reach HBM (config 5's teacher reads of
+    the navigation grid: the pool row, L2-resident) or where a kernel re-reads."""
+    if not traffic or not kernel_us:
+        return {"achieved_hbm_gbs": None, "hbm_frac": None}
+    gbs = traffic / (kernel_us * 1e-6) / 1e9
+    return {"achieved_hbm_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS}
 
 
 def profiled_kernel_us(fn, m, name):
@@ -538,6 +553,7 @@ def run(args):
                          "kernel_us_events": kernel_ms * 1e3, "ticks_per_launch": k_eff,
                          "bytes_per_launch": bps * n * k_eff, "bytes_per_env_step": bps,
                          "ceiling_gbs": ceiling_gbs, "frac_of_ceiling": achieved / ceiling_gbs,
+                         **hbm_rate(traffic, kernel_us_priced),
                          "ceiling": f"torch zero_ of each {R}-slot ring buffer in turn "
                                     f"({ceiling_slot_us:.1f} us per {ring[0].numel() * ring.element_size() / 1e6:.0f} MB "
                                     "slot), measured in this run before the timed region"},
@@ -649,10 +665,12 @@ def run_trainer(args):
     def receive(r):                                  # student.receive keeps the labels
         received.append(r)
 
+    fused = args.trainer_teacher == "fused"
+
     def rollout():
         received.clear()
         return do_rollout(sim, spec_d, act, False, behavior_clone=bc_d, receive=receive,
-                          lookahead=True, graph=args.rollout_graph)
+                          lookahead=fused, graph=args.rollout_graph, fused_teacher=fused)
 
     for _ in range(args.warmup):
         rollout()
@@ -693,7 +711,7 @@ def run_trainer(args):
     torch.cuda.synchronize()
     w0 = time.perf_counter()
     info = do_rollout(sim, spec_d, timed_act, False, behavior_clone=bc_d, receive=receive,
-                      lookahead=True)
+                      lookahead=fused, fused_teacher=fused)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - w0) / max(1, info.ticks)
     pol_us = float(np.mean([a.elapsed_time(b) for a, b in marks[:info.ticks]])) * 1e3
@@ -702,10 +720,10 @@ def run_trainer(args):
     sim.check()
     # the tick kernel's own device duration over one more rollout (as rocprof prices it: without
     # the dispatch gaps env_kernel above includes)
-    kname, kenvs, lanes = sim.step_shape(teach=True)
+    kname, kenvs, lanes = sim.step_shape(teach=fused)
     prof_us = None if args.no_kernel_profiler else profiled_kernel_us(
         lambda: do_rollout(sim, spec_d, act, False, behavior_clone=bc_d, receive=receive,
-                           lookahead=True), 1, kname)
+                           lookahead=fused, fused_teacher=fused), 1, kname)
     kernel_us = prof_us if prof_us else env_us
 
     if rank == 0:
@@ -713,7 +731,7 @@ def run_trainer(args):
         F = sim.n_features
         bps = bytes_per_env_step(sim.width, sim.height, win, F, True, 4)
         achieved = bps * n / (kernel_us * 1e-6) / 1e9
-        workload = f"{args.world}_w{win}_B{n}_trainer_closed_loop_train_fused_teacher"
+        workload = f"{args.world}_w{win}_B{n}_trainer_closed_loop_train_{args.trainer_teacher}_teacher"
         value = tot[1] / elapsed                     # live env-steps (num_interactions)
         line = {
             "metric": "env-steps/sec (whole node), 12x12 craft_medium, batch=65536",
@@ -737,7 +755,7 @@ def run_trainer(args):
                        "(ticks until every episode has ended, <= max_timesteps); value counts live "
                        "env-steps (num_interactions, imitation.py:54: envs not yet done), "
                        "slot_env_steps_per_s every env slot every tick", "lookahead": True,
-                       "rollout_graph_ticks": args.rollout_graph,
+                       "rollout_graph_ticks": args.rollout_graph, "teacher": args.trainer_teacher,
                        "parallelism": f"env-shard x{world_size}"},
             "slot_env_steps_per_s": tot[0] / elapsed,
             "dist": report,
@@ -755,7 +773,9 @@ def run_trainer(args):
             "roofline": {"bound": "latency (tick prologue + BFS beside the observation stream)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(args, workload, 1),
-                         "kernel": f"{kname} (craft_step_teach, {kenvs} envs, {lanes} teacher lanes)",
+                         **hbm_rate(pmc_traffic(args, workload, 1), kernel_us),
+                         "kernel": (f"{kname} (craft_step_teach, {kenvs} envs, {lanes} teacher lanes)" if fused
+                                    else f"{kname} (craft_step_ex, {kenvs} envs; craft_teacher beside act())"),
                          "kernel_us": kernel_us,
                          "kernel_us_source": ("torch profiler device records (as rocprof)" if prof_us
                                               else "HIP events: policy end to next policy start"),

@@ -76,6 +76,10 @@ struct SimView {
   // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16 | yield<<24.  Kernels copy the table to LDS.
   // (As kernel-argument words they cost ~50 scalar registers, which spilled.)
   const uint32_t* rcw;
+  // the same recipes grouped by workshop: [CRAFT_MAX_KINDS][kWsSlots] uint4 (the three recipe
+  // words and 0), slot j of kind k = the j-th recipe made at workshop k in dict order, all zero
+  // past the last; null when some workshop has more than kWsSlots recipes
+  const uint4* wsr;
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
 };
 
@@ -331,13 +335,21 @@ __device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, b
   return dy < 0 ? CRAFT_DOWN : dy > 0 ? CRAFT_UP : dx < 0 ? CRAFT_LEFT : CRAFT_RIGHT;
 }
 
+// Recipe slots per workshop kind in SimView::wsr (recipes.yaml: 3 per workshop).
+constexpr int kWsSlots = 4;
+
 // RCV: the recipe words also sit in a VGPR, lane w holding word w (w < 3 * CRAFT_MAX_RECIPES,
 // loaded while every lane of the wave was active); the recipe loop reads them with v_readlane
 // instead of one LDS round trip per recipe.
-template <bool RCV = false>
+// WSR: `wsr` is SimView::wsr copied to LDS (non-null): a lane at a workshop runs only that
+// workshop's recipes (per-lane words, the next slot read one ahead), each recipe one LDS round
+// trip for its ingredient and output counts, the updates applied in registers in the reference's
+// order and written once; instead of every recipe of every workshop some lane of the wave faces.
+template <bool RCV = false, bool WSR = false>
 __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
-                                           bool& mask_changed, uint32_t rcv = 0u, int64_t slot = -1) {
+                                           bool& mask_changed, uint32_t rcv = 0u, int64_t slot = -1,
+                                           const uint4* wsr = nullptr) {
   auto rword = [&](int w) -> uint32_t {
     if constexpr (RCV) return __builtin_amdgcn_readlane(rcv, w);
     else return __builtin_amdgcn_readfirstlane(rc[w]);
@@ -363,7 +375,48 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
           g[c] = 0;
           mask_set(m, c);
           inv_changed = mask_changed = true;
-#ifndef CRAFT_ABL_NORECIPE
+        } else if (WSR && cls == CRAFT_KIND_WORKSHOP) {   // recipes in dict order, craft.py:388-401
+          uint4 nxt = wsr[thing * kWsSlots];
+          for (int j = 0; j < kWsSlots; ++j) {
+            const uint4 w = nxt;
+            if ((int)((w.x >> 8) & 0xff) != thing) break;       // past this workshop's last recipe
+            if (j + 1 < kWsSlots) nxt = wsr[thing * kWsSlots + j + 1];
+            const int n_in = (w.x >> 16) & 0xff, out = w.x & 0xff;
+            const int k0 = w.x >> 24, k1 = (w.y >> 8) & 0xff, k2 = w.y >> 24, k3 = (w.z >> 8) & 0xff;
+            const int c0 = w.y & 0xff, c1 = (w.y >> 16) & 0xff, c2 = w.z & 0xff, c3 = (w.z >> 16) & 0xff;
+            int h0 = iv[k0], h1 = iv[k1], h2 = iv[k2], h3 = iv[k3], ho = iv[out];   // (unused slots: kind 0)
+            const bool have = (n_in < 1 || h0 >= c0) && (n_in < 2 || h1 >= c1) &&
+                              (n_in < 3 || h2 >= c2) && (n_in < 4 || h3 >= c3);
+            if (!have) continue;
+            // n_inventory[output] += yld, then each ingredient -= its count (craft.py:396-399), on
+            // register copies; copies of one kind are kept equal after every update
+            const int made = ho + (int)(w.z >> 24);
+            if (made > 255) latch_error(v.err, CRAFT_ERANGE, slot);   // u8 count would wrap: saturate
+            ho = made > 255 ? 255 : made;
+            h0 = k0 == out ? ho : h0; h1 = k1 == out ? ho : h1; h2 = k2 == out ? ho : h2; h3 = k3 == out ? ho : h3;
+            if (n_in > 0) {
+              h0 = (h0 - c0) & 0xff;
+              ho = out == k0 ? h0 : ho; h1 = k1 == k0 ? h0 : h1; h2 = k2 == k0 ? h0 : h2; h3 = k3 == k0 ? h0 : h3;
+            }
+            if (n_in > 1) {
+              h1 = (h1 - c1) & 0xff;
+              ho = out == k1 ? h1 : ho; h0 = k0 == k1 ? h1 : h0; h2 = k2 == k1 ? h1 : h2; h3 = k3 == k1 ? h1 : h3;
+            }
+            if (n_in > 2) {
+              h2 = (h2 - c2) & 0xff;
+              ho = out == k2 ? h2 : ho; h0 = k0 == k2 ? h2 : h0; h1 = k1 == k2 ? h2 : h1; h3 = k3 == k2 ? h2 : h3;
+            }
+            if (n_in > 3) {
+              h3 = (h3 - c3) & 0xff;
+              ho = out == k3 ? h3 : ho; h0 = k0 == k3 ? h3 : h0; h1 = k1 == k3 ? h3 : h1; h2 = k2 == k3 ? h3 : h2;
+            }
+            iv[out] = (uint8_t)ho;
+            if (n_in > 0) iv[k0] = (uint8_t)h0;
+            if (n_in > 1) iv[k1] = (uint8_t)h1;
+            if (n_in > 2) iv[k2] = (uint8_t)h2;
+            if (n_in > 3) iv[k3] = (uint8_t)h3;
+            inv_changed = true;
+          }
         } else if (cls == CRAFT_KIND_WORKSHOP) {     // recipes in dict order, craft.py:388-401
           // Recipe words are wave-uniform (LDS broadcast reads or v_readlane, kept in scalar
           // registers); a recipe's ingredient counts are read together, so a matching recipe
@@ -391,7 +444,6 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
             if (n_in > 3) iv[k3] = (uint8_t)(iv[k3] - c3);
             inv_changed = true;
           }
-#endif
         } else if (cls == CRAFT_KIND_WATER) {        // craft.py:403-406
           if (iv[v.bridge] > 0) {
             g[c] = 0;

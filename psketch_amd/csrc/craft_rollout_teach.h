@@ -23,8 +23,7 @@
 //     task's satisfies() predicates (craft_host.h hint_tables), three rounds of LDS loads;
 //   * a go[X] leaf on a grid the teacher table lists (the pool row minus a subset of its listed
 //     clearable cells) issues the table's answer load (LDS-DMA) and decodes it kRtLag walks later
-//     (policy actions; the data is in LDS by the end of its own walk, see fetch) or right away
-//     (label actions);
+//     (policy actions) or right away (label actions);
 //   * any other go[X] leaf becomes a BFS job: the leaf lane builds the band bitsets of its grid
 //     row while the row is still current and queues them in LDS;
 //   * between its own duties the wave runs the queued jobs, one BFS level per step on 16 quads
@@ -74,10 +73,11 @@ constexpr uint32_t kRtSpinCap = 1u << 22;
 // [2][TILE] | the tick's outputs [2][TILE][2] | task table [64] u16 | subtasks [64][4] | recipe
 // words [16][3] | control words [8] | label rows [8][4 + TILE] | BFS job queue [32][2 NW + 1] |
 // table requests [4][TILE] | their rows [4] | clearable cells [TILE][2] | hint table:
-// descriptors [64][4], leaf bytes [2048] | nibble positions [4][TILE]
+// descriptors [64][4], leaf bytes [2048] | nibble positions [4][TILE] | workshop recipes
+// [CRAFT_MAX_KINDS][kWsSlots] uint4 (SimView::wsr)
 struct RtLds {
   int grid, pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint,
-      tnib, bytes;
+      tnib, wsr, bytes;
 };
 __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -101,7 +101,8 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.tcell = l.tpend + kRtLag * 4;                          // [tile][2] each env's listed clearable cells
   l.hint = up16(l.tcell + tile * 8);                       // craft_host.h hint_tables
   l.tnib = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;   // [kRtLag][tile] nibble in the word
-  l.bytes = up16(l.tnib + kRtLag * tile);
+  l.wsr = up16(l.tnib + kRtLag * tile);
+  l.bytes = l.wsr + CRAFT_MAX_KINDS * kWsSlots * 16;
   return l;
 }
 // envs per tile: 32 for 3x3 windows (as the split rollout kernel), 16 for wider ones (their
@@ -138,6 +139,15 @@ __device__ __forceinline__ uint32_t rt_job_meta(int p0, int d0, int conn, int ro
          ((uint32_t)env << 15);
 }
 
+// Byte k (per lane) of an inventory row held in 8 registers.  Written as byte permutes, not as
+// r[k >> 2]: hipcc turns an indexed (or index-compared) word into a scratch array.
+__device__ __forceinline__ int rbyte(const uint32_t (&r)[8], int k) {
+  const uint32_t sel = 0x0c0c0c00u | (uint32_t)(k & 7);             // byte k & 7 of a word pair
+  const uint32_t p0 = __builtin_amdgcn_perm(r[1], r[0], sel), p1 = __builtin_amdgcn_perm(r[3], r[2], sel);
+  const uint32_t p2 = __builtin_amdgcn_perm(r[5], r[4], sel), p3 = __builtin_amdgcn_perm(r[7], r[6], sel);
+  const uint32_t q0 = (k & 8) ? p1 : p0, q1 = (k & 8) ? p3 : p2;
+  return (int)((k & 16) ? q1 : q0);
+}
 template <int WIN, int TILE, int NW>
 __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v, RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -170,6 +180,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
+  uint4* s_wsr = reinterpret_cast<uint4*>(smem + lay.wsr);               // SimView::wsr (when set)
   const uint4* s_hdesc = reinterpret_cast<const uint4*>(smem + lay.hint);   // [task]: predicates, leaf offset
   const uint8_t* s_hleaf = smem + lay.hint + CRAFT_MAX_TASKS * 16;
   // [0] the claimed unit, [1] barrier arrivals, [2] items whose labels are complete (label actions),
@@ -213,6 +224,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   for (int t = tid; t < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS; t += NT)
     s_tsub[t] = t < v.n_tasks * CRAFT_MAX_SUBTASKS ? v.task_sub[t] : 0;
   for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += NT) s_rc[t] = v.rcw[t];
+  if (v.wsr)
+    for (int t = tid; t < CRAFT_MAX_KINDS * kWsSlots; t += NT) s_wsr[t] = v.wsr[t];
   for (int t = tid; t < CRAFT_MAX_TASKS * 4 + ((v.hint_bytes + 3) >> 2); t += NT)
     reinterpret_cast<uint32_t*>(smem + lay.hint)[t] = v.hint[t];
   {
@@ -263,6 +276,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     uint3 c_hd = make_uint3(0u, 0u, 0u);                               // the task's hint descriptor
     uint2 c_cw = make_uint2(~0u, ~0u);                                 // the row's listed clearable cells
     int ncl = 0;                                                       // cells cleared this episode
+    // the inventory row after the last tick, read at its end (its latency behind the barrier, or
+    // shared with the label lookup) and written into the next tick's buffer, instead of a read of
+    // the other buffer at the tick's start
+    uint32_t ivn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     bool live = false, lsrc = false;
     int64_t slot = 0;
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(s_pristine + lane * GS);
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         }
         uint32_t* iv0 = reinterpret_cast<uint32_t*>(inv_of(0));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) iv0[i] = ivr[i];
+        for (int i = 0; i < 8; ++i) iv0[i] = ivn[i] = ivr[i];
         uint8_t* b0 = grid_of(0);
 #pragma unroll
         for (int w = 0; w < 8; ++w) {                                  // cells cleared this episode
@@ -380,11 +397,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     // ---- (label actions) the teacher's decision for this lane's new state, as the teacher wave's
     // walk makes it (D_WALK below: hint table leaf, then the nibble table's entry), or kCRow ----
     const bool c_tab = v.ttab4 != nullptr && v.ttab != nullptr && a.use_table;
-    auto c_label = [&](const uint8_t* gr, const uint8_t* ivb) __attribute__((always_inline)) -> uint32_t {
+    auto c_label = [&](const uint8_t* gr, const uint32_t (&ivw)[8]) __attribute__((always_inline)) -> uint32_t {
       if (s.frozen) return 0xffu;                                      // -1: the label of a done env
       const int facing = gr[(s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir))];
       const uint4 hd = make_uint4(c_hd.x, c_hd.y, c_hd.z, 0u);
-      const uint32_t* ivw = reinterpret_cast<const uint32_t*>(ivb);
       uint32_t have = 0;
 #pragma unroll
       for (int w = 0; w < 8; ++w) have |= byte_tops(nonzero_bytes(ivw[w])) << (4 * w);
@@ -492,12 +508,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           else if (chg) gr[chg - 1] = 0;
         }
         if (sync) {
-          const uint32_t* src = reinterpret_cast<const uint32_t*>(inv_of(k + 1));
-          uint32_t w[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) w[i] = src[i];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(iv)[i] = w[i];
+          for (int i = 0; i < 8; ++i) reinterpret_cast<uint32_t*>(iv)[i] = ivn[i];
         }
         sync = sync ? 2 : 1;
         chg = 0;
@@ -522,7 +534,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         if (d) {                                                       // satisfies() of the pre-step state
           const int goal = task_word & 0xf, arg = (task_word >> 4) & 0xff;
           const int fc = (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir));
-          if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) succ = iv[arg] > 0;
+          if (goal == CRAFT_GOAL_GET || goal == CRAFT_GOAL_MAKE) succ = rbyte(ivn, arg) > 0;
           else if (goal == CRAFT_GOAL_GO) succ = (int)gr[fc] == arg;
           else succ = -1;
         }
@@ -544,9 +556,10 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         const uint64_t tc2 = RT_CLK();
         if (!d) {
           bool inv_changed = false, mask_changed = false;
-          uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           const int fc = (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir));   // what USE clears
+          uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
+          else if (v.wsr) transition<true, true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot, s_wsr);
           else transition<true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot);
           if (mask_changed) {
             ++ncl;
@@ -559,7 +572,9 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         st = pack_state(s);
         RT_ACC(3, tc2);
         const uint64_t tc3 = RT_CLK();
-        if (lsync && lsrc && k + 1 < a.n_ticks) c_tag = c_label(gr, iv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ivn[i] = reinterpret_cast<const uint32_t*>(iv)[i];
+        if (lsync && lsrc && k + 1 < a.n_ticks) c_tag = c_label(gr, ivn);
         // done, success, reward and the recorded action (action_seqs, imitation.py:59-61) leave
         // from the streaming waves, one array each
         s_cout[(k & 1) * TILE + lane] = make_uint2((uint32_t)d | ((uint32_t)(succ + 1) << 1) | ((uint32_t)counted << 3) |
@@ -921,14 +936,16 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       return jtail != jhead || __ballot(q.ph != kQIdle) != 0;
     };
     // Policy actions: each walk fetches its items' table words with one LDS-DMA
-    // (__builtin_amdgcn_global_load_lds: the compiler sets M0 itself), a dummy one when the item
-    // asks for none, so that the fetch of the item kRtLag walks back is exactly the one
-    // vmcnt(kRtLag - 1) leaves waiting for (loads complete in order; any other VMEM op of this
-    // wave, a latched error, only makes the wait stricter).  hipcc cannot tell the DMA's target
-    // from the rest of the dynamic LDS, so it also waits vmcnt(0) before the wave's next LDS
-    // access: the fetch lands within its walk's interval instead of kRtLag walks later.  Measured
-    // against round 5's inline asm (which set M0 by hand): 398-400 against 391-392 us per 20-tick
-    // launch, 471 against 466-475 with label actions (profiles/r06/ab_dma).
+    // (global_load_lds_dword), a dummy one when the item asks for none, so that the fetch of the
+    // item kRtLag walks back is exactly the one vmcnt(kRtLag - 1) leaves waiting for (loads
+    // complete in order; any other VMEM op of this wave, a latched error, only makes the wait
+    // stricter).  One inline-asm statement that saves M0, points it at the slot, issues the DMA and
+    // restores M0: M0 is compiler-reserved, so no compiler-held M0 value may be lost across it
+    // (round 5's statement set M0 without restoring it).  Not __builtin_amdgcn_global_load_lds:
+    // hipcc cannot tell the DMA's target from the rest of the dynamic LDS, so it waits vmcnt(0)
+    // before the wave's next LDS access (28 more vmcnt(0) in rollout_teach_kernel<3, 32, 4>), which
+    // undoes the lag: config 5 402.5-405.6 against 393.2-395.4 us per 20-tick launch on one box
+    // (profiles/r06/ab_dma).  The "memory" clobber orders it against the slot's reads (decode_slot).
     // (the answers as 4-bit labels, SimView::ttab4: a quarter of the u16 table's footprint, so
     // more of the lines the gather touches are L2 hits; req is then the dword index)
     const bool nib = v.ttab4 != nullptr;
@@ -936,8 +953,13 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         nib ? (const void*)v.ttab4 : v.ttab ? (const void*)v.ttab : (const void*)v.task_tab);
     auto fetch = [&](int q, uint32_t req) __attribute__((always_inline)) {
       const uint32_t* gp = tbase + (req == ~0u ? 0u : nib ? req : req >> 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // the slot's last reads are done
-      __builtin_amdgcn_global_load_lds(gp, (__attribute__((address_space(3))) void*)(s_tval + q * 64), 4, 0, 0);
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)(s_tval + q * 64));
+      uint32_t keep;
+      // (lgkmcnt(0): the slot's last reads are done)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                   "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(gp), "s"(lds) : "memory");
     };
     // decode slot q's words (fetched kRtLag walks ago, or at the end: wait_all) into their label row
     auto decode_slot = [&](int q, bool wait_all) __attribute__((always_inline)) {

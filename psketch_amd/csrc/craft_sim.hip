@@ -141,6 +141,7 @@ struct craft_sim {
   uint8_t* d_pool = nullptr;
   uint8_t* d_pool_conn = nullptr;   // per pool row: free cells 4-connected (teacher shortcut)
   uint32_t* d_rcw = nullptr;
+  uint4* d_wsr = nullptr;           // SimView::wsr: the recipes grouped by workshop, or null
   uint64_t* d_state = nullptr;
   uint32_t* d_init = nullptr;
   uint4* d_inv = nullptr;
@@ -441,6 +442,20 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
       rcw[3 * r + q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) | ((uint32_t)b[4 * q + 2] << 16) |
                        ((uint32_t)b[4 * q + 3] << 24);
   }
+  // SimView::wsr: workshop k's recipes in dict order, kWsSlots slots per kind (none past that)
+  std::vector<uint4> wsr((size_t)CRAFT_MAX_KINDS * craft::kWsSlots, make_uint4(0, 0, 0, 0));
+  bool wsr_ok = true;
+  {
+    int used[CRAFT_MAX_KINDS] = {};
+    for (int r = 0; r < cfg->n_recipes; ++r) {
+      const int k = cfg->recipe[r].workshop;
+      if (k <= 0 || k >= CRAFT_MAX_KINDS || used[k] >= craft::kWsSlots) {
+        wsr_ok = false;
+        continue;
+      }
+      wsr[(size_t)k * craft::kWsSlots + used[k]++] = make_uint4(rcw[3 * r], rcw[3 * r + 1], rcw[3 * r + 2], 0u);
+    }
+  }
   std::vector<uint16_t> task_tab(CRAFT_MAX_TASKS, 0);
   std::vector<int32_t> task_sub(CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS, 0);
   craft_host::task_tables(*cfg, task_tab.data(), task_sub.data());
@@ -470,6 +485,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_mask, 2 * sizeof(uint4) * n_envs);
   ALLOC(s->d_task, sizeof(uint16_t) * task_tab.size());
   ALLOC(s->d_rcw, sizeof(rcw));
+  if (wsr_ok) ALLOC(s->d_wsr, sizeof(uint4) * wsr.size());
   ALLOC(s->d_task_sub, sizeof(int32_t) * task_sub.size());
   ALLOC(s->d_hint, hint_bytes);
   ALLOC(s->d_stats, 4 * sizeof(int64_t) * s->n_tiles);
@@ -503,6 +519,8 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     return cleanup(e, "task table");
   if ((e = hipMemcpy(s->d_rcw, rcw, sizeof(rcw), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "recipe table");
+  if (s->d_wsr && (e = hipMemcpy(s->d_wsr, wsr.data(), sizeof(uint4) * wsr.size(), hipMemcpyHostToDevice)) != hipSuccess)
+    return cleanup(e, "workshop recipe table");
   if ((e = hipMemcpy(s->d_task_sub, task_sub.data(), sizeof(int32_t) * task_sub.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "subtask table");
   if ((e = hipMemcpy(s->d_hint, hint.data(), hint_bytes, hipMemcpyHostToDevice)) != hipSuccess)
@@ -548,6 +566,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     else v.kc_hi |= cls << (4 * (k - 16));
   }
   v.rcw = s->d_rcw;
+  v.wsr = s->d_wsr;
   *out = s;
   return CRAFT_OK;
 }
@@ -639,6 +658,7 @@ int craft_sim_destroy(craft_sim_t* s) {
   (void)hipFree(s->d_mask);
   (void)hipFree(s->d_task);
   (void)hipFree(s->d_rcw);
+  (void)hipFree(s->d_wsr);
   (void)hipFree(s->d_task_sub);
   (void)hipFree(s->d_hint);
   (void)hipFree(s->d_stats);

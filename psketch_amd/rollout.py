@@ -80,7 +80,9 @@ def do_rollout(sim, spec, act, is_eval, behavior_clone=None, receive=None, keep_
       loop and the distances/summary phases (each ends at a device sync).
     fused_teacher: when not is_eval, each tick's step also labels the new states
       (craft_step_teach: the next tick's ref_actions, in the same launch);
-      False runs craft_teacher on a side stream, overlapping the student.
+      False runs craft_teacher on a side stream, overlapping the student (with graph=G the
+      fork and join are captured in the graphs: the teacher of tick t's states beside act(t),
+      then craft_step_ex).
     lookahead: the all(done) test of tick t (imitation.py:42) no longer blocks the
       host before tick t + 1 is queued: tick t + 1 (act and step) is queued behind tick
       t's event, and only then is tick t's any-live flag read.  When tick t ended every episode the queued tick is discarded: its step
@@ -253,8 +255,6 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
     n, dev, T = sim.n_envs, sim.device, sim.config.max_timesteps
     if keep_obs:
         raise ValueError("graph mode does not keep observations (keep_obs)")
-    if not is_eval and not fused_teacher:
-        raise ValueError("graph mode needs is_eval or fused_teacher")
     if G < 1:
         raise ValueError("graph: ticks per graph must be positive")
     if T <= 0:
@@ -265,7 +265,8 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
     if not flag_dev:
         raise RuntimeError("graph mode needs the any-live flags in mapped host memory")
     gs = getattr(sim, "_graph_state", None)
-    key = (is_eval, G, T, graph_key)
+    side_teacher = not is_eval and not fused_teacher
+    key = (is_eval, G, T, graph_key, side_teacher)
     if gs is None or not _same_act(gs["act"], act) or gs["key"] != key:
         sim._graph_state = None                  # drop the old graphs before capturing new ones
         gs = sim._graph_state = {
@@ -284,15 +285,30 @@ def _graph_rollout(sim, spec, act, is_eval, behavior_clone, receive, keep_obs, t
         sim.teacher(action_out=refs[0])          # the initial states' labels; then every step's
     nch = (T + G - 1) // G
     if not gs["graphs"]:
-        step = _stepper(sim, not is_eval, gs["bc"], success)
+        step = _stepper(sim, not is_eval and not side_teacher, gs["bc"], success)
+        main = torch.cuda.current_stream(dev)
+        side = None
+        if side_teacher:                         # created once per simulator (costly)
+            side = getattr(sim, "_teacher_stream", None)
+            if side is None:
+                side = sim._teacher_stream = torch.cuda.Stream(dev)
 
         def issue(t):
+            # (side teacher) tick t's ref_actions, the labels of the states tick t - 1 left, on a
+            # forked stream beside the student's act(t); the step joins it (tick 0's come from
+            # the eager call before the loop)
+            cur = torch.cuda.current_stream(dev)    # (the capture's stream)
+            if side is not None and t > 0:
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    sim.teacher(action_out=refs[t])
             actions = act(obs, t)
             actions = actions.to(device=dev, dtype=torch.int32).reshape(n).contiguous()
+            if side is not None and t > 0:
+                cur.wait_stream(side)
             step(t, actions, obs, None if is_eval else refs[t], seqs[t], flag_dev + 4 * t,
-                 None if is_eval else refs[t + 1])
+                 None if is_eval or side is not None else refs[t + 1])
 
-        main = torch.cuda.current_stream(dev)
         warm = torch.cuda.Stream(dev)            # the student's libraries warmed off the capture
         warm.wait_stream(main)
         with torch.cuda.stream(warm):

@@ -183,13 +183,15 @@ def test_host_flag_pointer(gpu):
     assert N.lib().craft_host_flag_pointer(plain.data_ptr(), ctypes.byref(p)) == N.EINVAL
 
 
-@pytest.mark.parametrize("is_eval,bc_rate,stop_at,G", [(False, 0.5, None, 8), (False, 0.0, 6, 7),
-                                                       (True, 0.0, 9, 40), (False, 0.0, 17, 1)])
-def test_graph_rollout_equals_sync_loop(gpu, is_eval, bc_rate, stop_at, G):
+@pytest.mark.parametrize("is_eval,bc_rate,stop_at,G,fused", [(False, 0.5, None, 8, True), (False, 0.0, 6, 7, True),
+                                                             (True, 0.0, 9, 40, True), (False, 0.0, 17, 1, True),
+                                                             (False, 0.5, None, 8, False), (False, 1.0, 13, 5, False)])
+def test_graph_rollout_equals_sync_loop(gpu, is_eval, bc_rate, stop_at, G, fused):
     """do_rollout(graph=G) (HIP graphs of G ticks, captured once per simulator and act, replayed
     by later rollouts) gives the synchronous loop's result bit for bit at 65,536 envs: two
     rollouts on different specs and cloning masks through the same graphs, early stops inside
-    and at the end of a chunk, every receive() call."""
+    and at the end of a chunk, every receive() call; fused=False: the teacher forked beside the
+    student inside the graphs (against the fused synchronous loop)."""
     from psketch_amd import CraftSim
     from psketch_amd.rollout import do_rollout
     from psketch_amd.sim import sample_scenarios, synthetic_specs
@@ -217,10 +219,13 @@ def test_graph_rollout_equals_sync_loop(gpu, is_eval, bc_rate, stop_at, G):
         for sim, graph in ((ref_sim, 0), (g_sim, G)):
             received = []
             info = do_rollout(sim, spec, act, is_eval, behavior_clone=bc,
-                              receive=lambda r: received.append(r.cpu().numpy()), graph=graph)
+                              receive=lambda r: received.append(r.cpu().numpy()), graph=graph,
+                              fused_teacher=fused or not graph)
             outs.append((info, received))
         (a, ra), (b, rb) = outs
-        assert a.ticks == b.ticks == (stop_at + 1 if stop_at is not None else cfg.max_timesteps)
+        assert a.ticks == b.ticks
+        if bc_rate < 1:                              # (every env cloning: the student's STOP is never taken)
+            assert a.ticks == (stop_at + 1 if stop_at is not None else cfg.max_timesteps)
         for k in ("action_seqs", "n_actions", "success", "distances", "is_get"):
             assert torch.equal(getattr(a, k), getattr(b, k)), (rep, k)
         assert (a.num_interactions, a.num_steps) == (b.num_interactions, b.num_steps)

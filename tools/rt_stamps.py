@@ -16,6 +16,10 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 LIB = os.path.join(REPO, "psketch_amd", "lib", "libpsketch_craft_rtst.so")
+if "--lib" in sys.argv:                  # another stamped build (tools/diag_build.py --out NAME)
+    i = sys.argv.index("--lib")
+    LIB = os.path.join(REPO, "psketch_amd", "lib", sys.argv[i + 1])
+    del sys.argv[i:i + 2]
 
 if "--build" in sys.argv:
     sys.path.insert(0, os.path.join(REPO, "tools"))
