@@ -345,11 +345,14 @@ constexpr int kWsSlots = 4;
 // workshop's recipes (per-lane words, the next slot read one ahead), each recipe one LDS round
 // trip for its ingredient and output counts, the updates applied in registers in the reference's
 // order and written once; instead of every recipe of every workshop some lane of the wave faces.
-template <bool RCV = false, bool WSR = false>
+// NB: `nbw` holds the kinds of the agent's four neighbour cells (byte d: the cell one step in
+// direction d, DOWN UP LEFT RIGHT), read before the tick: the facing cell and a move's target
+// without a grid read.
+template <bool RCV = false, bool WSR = false, bool NB = false>
 __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
                                            bool& mask_changed, uint32_t rcv = 0u, int64_t slot = -1,
-                                           const uint4* wsr = nullptr) {
+                                           const uint4* wsr = nullptr, uint32_t nbw = 0u) {
   auto rword = [&](int w) -> uint32_t {
     if constexpr (RCV) return __builtin_amdgcn_readlane(rcv, w);
     else return __builtin_amdgcn_readfirstlane(rc[w]);
@@ -366,7 +369,7 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
                     (d == CRAFT_RIGHT && s.x < v.W - 1) || (d == CRAFT_UP && s.y < H - 1);
     if (ok) {
       const int c = (s.x + dir_dx(d)) * H + (s.y + dir_dy(d));
-      const int thing = g[c];
+      const int thing = NB ? (int)((nbw >> (8 * d)) & 0xffu) : g[c];
       if (thing != 0) {
         const int cls = kind_class(v, thing);
         if (cls == CRAFT_KIND_GRABBABLE) {           // craft.py:383-386
@@ -464,7 +467,7 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
   // Collision against the pre-action grid (craft.py:418-421); USE/STOP do not move.
   if (dx | dy) {
     const int nx = s.x + dx, ny = s.y + dy;
-    if (g[nx * H + ny] == 0) { s.x = nx; s.y = ny; }
+    if ((NB ? (nbw >> (8 * a)) & 0xffu : g[nx * H + ny]) == 0) { s.x = nx; s.y = ny; }
   }
   s.dir = ndir;
 }

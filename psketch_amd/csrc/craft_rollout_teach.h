@@ -266,6 +266,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     uint64_t st = 0;
     uint32_t init_word = 0, task_word = 0, conn = 0;
     uint32_t clr = 0, clr_prev = 0, chg = 0;
+    uint32_t clk = 0, clk_prev = 0;   // the kinds of clr's (up to 3) cells before they were cleared
     constexpr uint32_t kRestart = 0x80000000u;
     int sync = 0, lab0 = 0;
     // (label actions) the label of the state the last tick made, looked up by this wave itself:
@@ -280,13 +281,21 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     // shared with the label lookup) and written into the next tick's buffer, instead of a read of
     // the other buffer at the tick's start
     uint32_t ivn[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // the kinds of the agent's four neighbour cells after the last tick (transition NB, byte d:
+    // one step in direction d), read with ivn: the tick's facing cell / move target and the label
+    // lookup's facing cell without a grid read on the tick's path
+    uint32_t nbw = 0;
     bool live = false, lsrc = false;
     int64_t slot = 0;
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(s_pristine + lane * GS);
     const uint8_t* pr = s_pristine + lane * GS;
     auto grid_of = [&](int p) __attribute__((always_inline)) { return s_grid + (p & 1) * TILE * GS + lane * GS; };
+    auto read_nb = [&](const uint8_t* g) __attribute__((always_inline)) {
+      const int p = s.x * H + s.y;                                    // DOWN, UP, LEFT, RIGHT (craft.py:77-91)
+      nbw = (uint32_t)g[p - 1] | ((uint32_t)g[p + 1] << 8) | ((uint32_t)g[p - H] << 16) | ((uint32_t)g[p + H] << 24);
+    };
     auto inv_of = [&](int p) __attribute__((always_inline)) { return s_inv + (p & 1) * TILE * kInvStride + lane * kInvStride; };
-    auto restore = [&](uint8_t* g, uint32_t cl) __attribute__((always_inline)) {
+    auto restore = [&](uint8_t* g, uint32_t cl, uint32_t ck) __attribute__((always_inline)) {
       if (cl >> 31) {
         uint32_t* gw = reinterpret_cast<uint32_t*>(g);
         for (int q0 = 0; q0 < (v.CS >> 2); q0 += 12) {
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         for (int i = 0; i < 3; ++i)
           if (i < nc) {
             const int c = (cl >> (8 * i)) & 0xff;
-            g[c] = pr[c];
+            g[c] = (uint8_t)(ck >> (8 * i));                         // (no read of the pristine row)
           }
       }
     };
@@ -338,6 +347,8 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       chg = 0;
       clr = 0;
       clr_prev = 0;
+      clk = 0;
+      clk_prev = 0;
       sync = 0;
       if (live) {
         task_word = s_task[s.task];
@@ -384,11 +395,13 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
             const int cc = w * 32 + __ffs(mm) - 1;
             b0[cc] = 0;
             const uint32_t nc = (clr >> 24) & 3;
+            if (!(clr >> 31) && nc < 3) clk |= (uint32_t)pr[cc] << (8 * nc);
             clr = (clr >> 31) ? clr
                 : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)cc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
             mm &= mm - 1;
           }
         }
+        read_nb(b0);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -399,7 +412,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     const bool c_tab = v.ttab4 != nullptr && v.ttab != nullptr && a.use_table;
     auto c_label = [&](const uint8_t* gr, const uint32_t (&ivw)[8]) __attribute__((always_inline)) -> uint32_t {
       if (s.frozen) return 0xffu;                                      // -1: the label of a done env
-      const int facing = gr[(s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir))];
+      const int facing = (int)((nbw >> (8 * s.dir)) & 0xffu);
       const uint4 hd = make_uint4(c_hd.x, c_hd.y, c_hd.z, 0u);
       uint32_t have = 0;
 #pragma unroll
@@ -504,7 +517,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
               if (q0 + j < (v.CS >> 2)) gw[q0 + j] = w[j];
           }
         } else if (sync == 2) {
-          if (chg == kRestart) restore(gr, clr_prev);
+          if (chg == kRestart) restore(gr, clr_prev, clk_prev);
           else if (chg) gr[chg - 1] = 0;
         }
         if (sync) {
@@ -543,9 +556,11 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           s.timer = v.maxT;
 #pragma unroll
           for (int w = 0; w < 8; ++w) reinterpret_cast<uint32_t*>(iv)[w] = 0u;
-          restore(gr, clr);
+          restore(gr, clr, clk);
           clr_prev = clr;
+          clk_prev = clk;
           clr = 0;
+          clk = 0;
           chg = kRestart;
           ncl = 0;
         } else if (d && !s.frozen) {
@@ -559,12 +574,13 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           const int fc = (s.x + dir_dx(s.dir)) * H + (s.y + dir_dy(s.dir));   // what USE clears
           uint32_t m_unused[8] = {0, 0, 0, 0, 0, 0, 0, 0};
           if (act < 0 || act >= CRAFT_N_ACTIONS) latch_error(v.err, CRAFT_EBADACTION, slot);
-          else if (v.wsr) transition<true, true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot, s_wsr);
-          else transition<true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot);
+          else if (v.wsr) transition<true, true, true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot, s_wsr, nbw);
+          else transition<true, false, true>(v, s_rc, gr, iv, s, m_unused, act, inv_changed, mask_changed, rcv, slot, nullptr, nbw);
           if (mask_changed) {
             ++ncl;
             chg = 1u + (uint32_t)fc;
             const uint32_t nc = (clr >> 24) & 3;
+            if (!(clr >> 31) && nc < 3) clk |= ((nbw >> (8 * s.dir)) & 0xffu) << (8 * nc);   // USE cleared the facing cell
             clr = (clr >> 31) ? clr
                 : nc < 3 ? ((clr & 0x00ffffffu) | ((uint32_t)fc << (8 * nc)) | ((nc + 1) << 24)) : (1u << 31);
           }
@@ -574,6 +590,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         const uint64_t tc3 = RT_CLK();
 #pragma unroll
         for (int i = 0; i < 8; ++i) ivn[i] = reinterpret_cast<const uint32_t*>(iv)[i];
+        read_nb(gr);
         if (lsync && lsrc && k + 1 < a.n_ticks) c_tag = c_label(gr, ivn);
         // done, success, reward and the recorded action (action_seqs, imitation.py:59-61) leave
         // from the streaming waves, one array each
