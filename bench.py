@@ -97,6 +97,9 @@ def parse(argv=None):
                         "scripted policy's states), every env acting on its own label "
                         "(make_data.get_reference_actions' demonstrations at scale, auto-reset), or "
                         "behaviour cloning on a fixed half of the envs (imitation.py:56-57)")
+    p.add_argument("--teach-table", choices=("auto", "always", "never"), default="auto",
+                   help="teacher workload: which teachers read the teacher table (craft_sim_tune_teach "
+                        "table 0 / 1 / 2); results are identical")
     p.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     p.add_argument("--world", default="craft_medium_12x12")
     p.add_argument("--pool", type=int, default=1024)
@@ -363,6 +366,7 @@ def run(args):
         obs_store = 1 if args.workload == "teacher" and args.ticks_per_launch > 1 else 2
     sim.set_obs_format(args.obs_format)
     sim.tune_rollout(args.rollout_chunk, args.rollout_threads)
+    sim.tune_teach(0, 0, ("auto", "always", "never").index(args.teach_table))
     tasks = [t.id for t in sim.task_manager.dataset_tasks()]
     specs = synthetic_specs(grids, sim.width, sim.height, n, env_base, seed=args.seed,
                             task_ids=tasks)
@@ -543,7 +547,7 @@ def run(args):
                             "obs_ring": args.ring, "pool": args.pool,
                             "parallelism": f"env-shard x{world_size}",
                             "max_timesteps": sim.config.max_timesteps, "ticks_per_launch": K,
-                            "launches": len(timed_plan),
+                            "launches": len(timed_plan), "teach_table": args.teach_table,
                             "obs_store": ["write-back", "nontemporal", "sc1"][obs_store]}, **shape),
             "roofline": {"bound": bound, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,

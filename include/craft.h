@@ -190,10 +190,8 @@ int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t thread
  *           load for pool_capacity rows with m chosen to fit 1 GiB (12x12 craft_medium: m = 6,
  *           453 MB for 1024 rows); a loaded row's entries are built by the next launch that reads
  *           the table, on its stream, which then waits for them (craft_sim_sync_table)), for envs
- *           whose grid it lists: 0 (default) = auto
- *           (craft_step_teach only when its launch rewrites the previous launch's observation
- *           buffer, where the reads hit the Infinity Cache; every other teacher always),
- *           1 = always, 2 = never (every query runs the BFS). */
+ *           whose grid it lists: 0 (default) = auto (every teacher: measured faster in every
+ *           launch shape since the 4-bit copy), 1 = always, 2 = never (every query runs the BFS). */
 int craft_sim_tune_teach(craft_sim_t* sim, int32_t kernel, int32_t lanes, int32_t table);
 
 /* Host worker threads of the CPU variant of this ABI (libpsketch_craft_cpu.so), which splits

@@ -76,10 +76,12 @@ struct SimView {
   // count1<<16 | kind2<<24, count2 | kind3<<8 | count3<<16 | yield<<24.  Kernels copy the table to LDS.
   // (As kernel-argument words they cost ~50 scalar registers, which spilled.)
   const uint32_t* rcw;
-  // the same recipes grouped by workshop: [CRAFT_MAX_KINDS][kWsSlots] uint4 (the three recipe
-  // words and 0), slot j of kind k = the j-th recipe made at workshop k in dict order, all zero
-  // past the last; null when some workshop has more than kWsSlots recipes
-  const uint4* wsr;
+  // the same recipes grouped by workshop, compact: [CRAFT_MAX_KINDS][4] uint2, slot j < kWsSlots
+  // of kind k = the j-th recipe made at workshop k in dict order, {out | ws << 8 | in0 << 16 |
+  // in1 << 24, count0 | count1 << 8 | yield << 16} (an absent ingredient: kind 0, count 0), all
+  // zero past the last; null when a workshop has more than kWsSlots recipes or a recipe more
+  // than two ingredients (recipes.yaml: three per workshop, one or two ingredients)
+  const uint2* wsr;
   uint64_t* stamps;           // diagnostic builds only (CRAFT_STAMPS); null otherwise
 };
 
@@ -336,15 +338,17 @@ __device__ __forceinline__ int transition_code(int ox, int oy, const Agent& s, b
 }
 
 // Recipe slots per workshop kind in SimView::wsr (recipes.yaml: 3 per workshop).
-constexpr int kWsSlots = 4;
+constexpr int kWsSlots = 3;
 
 // RCV: the recipe words also sit in a VGPR, lane w holding word w (w < 3 * CRAFT_MAX_RECIPES,
 // loaded while every lane of the wave was active); the recipe loop reads them with v_readlane
 // instead of one LDS round trip per recipe.
 // WSR: `wsr` is SimView::wsr copied to LDS (non-null): a lane at a workshop runs only that
-// workshop's recipes (per-lane words, the next slot read one ahead), each recipe one LDS round
-// trip for its ingredient and output counts, the updates applied in registers in the reference's
-// order and written once; instead of every recipe of every workshop some lane of the wave faces.
+// workshop's recipes, in two LDS round trips whatever the recipe count (the slots' words, then
+// every slot's output and ingredient counts), the updates applied in registers in the
+// reference's order (an applied recipe's new counts forwarded to the later slots that name the
+// same kinds) and written once; instead of every recipe of every workshop some lane of the wave
+// faces, one or two round trips each.
 // NB: `nbw` holds the kinds of the agent's four neighbour cells (byte d: the cell one step in
 // direction d, DOWN UP LEFT RIGHT), read before the tick: the facing cell and a move's target
 // without a grid read.
@@ -352,7 +356,7 @@ template <bool RCV = false, bool WSR = false, bool NB = false>
 __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc, uint8_t* g, uint8_t* iv, Agent& s,
                                            uint32_t (&m)[8], int a, bool& inv_changed,
                                            bool& mask_changed, uint32_t rcv = 0u, int64_t slot = -1,
-                                           const uint4* wsr = nullptr, uint32_t nbw = 0u) {
+                                           const uint2* wsr = nullptr, uint32_t nbw = 0u) {
   auto rword = [&](int w) -> uint32_t {
     if constexpr (RCV) return __builtin_amdgcn_readlane(rcv, w);
     else return __builtin_amdgcn_readfirstlane(rc[w]);
@@ -379,46 +383,47 @@ __device__ __forceinline__ void transition(const SimView& v, const uint32_t* rc,
           mask_set(m, c);
           inv_changed = mask_changed = true;
         } else if (WSR && cls == CRAFT_KIND_WORKSHOP) {   // recipes in dict order, craft.py:388-401
-          uint4 nxt = wsr[thing * kWsSlots];
+          uint2 w[kWsSlots];
+#pragma unroll
+          for (int j = 0; j < kWsSlots; ++j) w[j] = wsr[thing * 4 + j];
+          int h[kWsSlots][3];                                    // counts of out, in0, in1 (kind 0: absent)
+#pragma unroll
           for (int j = 0; j < kWsSlots; ++j) {
-            const uint4 w = nxt;
-            if ((int)((w.x >> 8) & 0xff) != thing) break;       // past this workshop's last recipe
-            if (j + 1 < kWsSlots) nxt = wsr[thing * kWsSlots + j + 1];
-            const int n_in = (w.x >> 16) & 0xff, out = w.x & 0xff;
-            const int k0 = w.x >> 24, k1 = (w.y >> 8) & 0xff, k2 = w.y >> 24, k3 = (w.z >> 8) & 0xff;
-            const int c0 = w.y & 0xff, c1 = (w.y >> 16) & 0xff, c2 = w.z & 0xff, c3 = (w.z >> 16) & 0xff;
-            int h0 = iv[k0], h1 = iv[k1], h2 = iv[k2], h3 = iv[k3], ho = iv[out];   // (unused slots: kind 0)
-            const bool have = (n_in < 1 || h0 >= c0) && (n_in < 2 || h1 >= c1) &&
-                              (n_in < 3 || h2 >= c2) && (n_in < 4 || h3 >= c3);
-            if (!have) continue;
+            h[j][0] = iv[w[j].x & 0xff];
+            h[j][1] = iv[(w[j].x >> 16) & 0xff];
+            h[j][2] = iv[w[j].x >> 24];
+          }
+#pragma unroll
+          for (int j = 0; j < kWsSlots; ++j) {
+            if ((int)((w[j].x >> 8) & 0xff) != thing) continue;   // (the valid slots are a prefix)
+            const int out = w[j].x & 0xff, ka = (w[j].x >> 16) & 0xff, kb = w[j].x >> 24;
+            const int ca = w[j].y & 0xff, cb = (w[j].y >> 8) & 0xff;
+            int ho = h[j][0], ha = h[j][1], hb = h[j][2];
+            if (ha < ca || hb < cb) continue;
             // n_inventory[output] += yld, then each ingredient -= its count (craft.py:396-399), on
             // register copies; copies of one kind are kept equal after every update
-            const int made = ho + (int)(w.z >> 24);
+            const int made = ho + (int)((w[j].y >> 16) & 0xff);
             if (made > 255) latch_error(v.err, CRAFT_ERANGE, slot);   // u8 count would wrap: saturate
             ho = made > 255 ? 255 : made;
-            h0 = k0 == out ? ho : h0; h1 = k1 == out ? ho : h1; h2 = k2 == out ? ho : h2; h3 = k3 == out ? ho : h3;
-            if (n_in > 0) {
-              h0 = (h0 - c0) & 0xff;
-              ho = out == k0 ? h0 : ho; h1 = k1 == k0 ? h0 : h1; h2 = k2 == k0 ? h0 : h2; h3 = k3 == k0 ? h0 : h3;
-            }
-            if (n_in > 1) {
-              h1 = (h1 - c1) & 0xff;
-              ho = out == k1 ? h1 : ho; h0 = k0 == k1 ? h1 : h0; h2 = k2 == k1 ? h1 : h2; h3 = k3 == k1 ? h1 : h3;
-            }
-            if (n_in > 2) {
-              h2 = (h2 - c2) & 0xff;
-              ho = out == k2 ? h2 : ho; h0 = k0 == k2 ? h2 : h0; h1 = k1 == k2 ? h2 : h1; h3 = k3 == k2 ? h2 : h3;
-            }
-            if (n_in > 3) {
-              h3 = (h3 - c3) & 0xff;
-              ho = out == k3 ? h3 : ho; h0 = k0 == k3 ? h3 : h0; h1 = k1 == k3 ? h3 : h1; h2 = k2 == k3 ? h3 : h2;
-            }
+            ha = ka == out ? ho : ha;
+            hb = kb == out ? ho : hb;
+            ha = (ha - ca) & 0xff;
+            ho = out == ka ? ha : ho;
+            hb = kb == ka ? ha : hb;
+            hb = (hb - cb) & 0xff;
+            ho = out == kb ? hb : ho;
+            ha = ka == kb ? hb : ha;
             iv[out] = (uint8_t)ho;
-            if (n_in > 0) iv[k0] = (uint8_t)h0;
-            if (n_in > 1) iv[k1] = (uint8_t)h1;
-            if (n_in > 2) iv[k2] = (uint8_t)h2;
-            if (n_in > 3) iv[k3] = (uint8_t)h3;
+            iv[ka] = (uint8_t)ha;                                // (kind 0 absent: its own unchanged 0)
+            iv[kb] = (uint8_t)hb;
             inv_changed = true;
+#pragma unroll
+            for (int j2 = j + 1; j2 < kWsSlots; ++j2)            // forward the new counts
+#pragma unroll
+              for (int q = 0; q < 3; ++q) {
+                const int kq = q == 0 ? (int)(w[j2].x & 0xff) : q == 1 ? (int)((w[j2].x >> 16) & 0xff) : (int)(w[j2].x >> 24);
+                h[j2][q] = kq == out ? ho : kq == ka ? ha : kq == kb ? hb : h[j2][q];
+              }
           }
         } else if (cls == CRAFT_KIND_WORKSHOP) {     // recipes in dict order, craft.py:388-401
           // Recipe words are wave-uniform (LDS broadcast reads or v_readlane, kept in scalar

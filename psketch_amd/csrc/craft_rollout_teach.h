@@ -74,7 +74,7 @@ constexpr uint32_t kRtSpinCap = 1u << 22;
 // words [16][3] | control words [8] | label rows [8][4 + TILE] | BFS job queue [32][2 NW + 1] |
 // table requests [4][TILE] | their rows [4] | clearable cells [TILE][2] | hint table:
 // descriptors [64][4], leaf bytes [2048] | nibble positions [4][TILE] | workshop recipes
-// [CRAFT_MAX_KINDS][kWsSlots] uint4 (SimView::wsr)
+// [CRAFT_MAX_KINDS][4] uint2 (SimView::wsr)
 struct RtLds {
   int grid, pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint,
       tnib, wsr, bytes;
@@ -102,7 +102,7 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.hint = up16(l.tcell + tile * 8);                       // craft_host.h hint_tables
   l.tnib = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;   // [kRtLag][tile] nibble in the word
   l.wsr = up16(l.tnib + kRtLag * tile);
-  l.bytes = l.wsr + CRAFT_MAX_KINDS * kWsSlots * 16;
+  l.bytes = l.wsr + CRAFT_MAX_KINDS * 4 * 8;
   return l;
 }
 // envs per tile: 32 for 3x3 windows (as the split rollout kernel), 16 for wider ones (their
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
-  uint4* s_wsr = reinterpret_cast<uint4*>(smem + lay.wsr);               // SimView::wsr (when set)
+  uint2* s_wsr = reinterpret_cast<uint2*>(smem + lay.wsr);               // SimView::wsr (when set)
   const uint4* s_hdesc = reinterpret_cast<const uint4*>(smem + lay.hint);   // [task]: predicates, leaf offset
   const uint8_t* s_hleaf = smem + lay.hint + CRAFT_MAX_TASKS * 16;
   // [0] the claimed unit, [1] barrier arrivals, [2] items whose labels are complete (label actions),
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     s_tsub[t] = t < v.n_tasks * CRAFT_MAX_SUBTASKS ? v.task_sub[t] : 0;
   for (int t = tid; t < CRAFT_MAX_RECIPES * 3; t += NT) s_rc[t] = v.rcw[t];
   if (v.wsr)
-    for (int t = tid; t < CRAFT_MAX_KINDS * kWsSlots; t += NT) s_wsr[t] = v.wsr[t];
+    for (int t = tid; t < CRAFT_MAX_KINDS * 4; t += NT) s_wsr[t] = v.wsr[t];
   for (int t = tid; t < CRAFT_MAX_TASKS * 4 + ((v.hint_bytes + 3) >> 2); t += NT)
     reinterpret_cast<uint32_t*>(smem + lay.hint)[t] = v.hint[t];
   {

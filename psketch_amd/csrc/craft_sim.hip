@@ -141,7 +141,7 @@ struct craft_sim {
   uint8_t* d_pool = nullptr;
   uint8_t* d_pool_conn = nullptr;   // per pool row: free cells 4-connected (teacher shortcut)
   uint32_t* d_rcw = nullptr;
-  uint4* d_wsr = nullptr;           // SimView::wsr: the recipes grouped by workshop, or null
+  uint2* d_wsr = nullptr;           // SimView::wsr: the recipes grouped by workshop, or null
   uint64_t* d_state = nullptr;
   uint32_t* d_init = nullptr;
   uint4* d_inv = nullptr;
@@ -165,7 +165,6 @@ struct craft_sim {
   int teach_table = 0;
   bool hint_walk = false;           // some task keeps the hint walk (no hint table: craft_host.h)
   int teach_lanes = 0;
-  const void* last_teach_obs = nullptr;
   int32_t tt_kinds[16] = {};        // its slots' target kinds
   SimView view{};
   int tile = craft::kMaxTileEnvs;   // envs per tile workgroup
@@ -442,18 +441,23 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
       rcw[3 * r + q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) | ((uint32_t)b[4 * q + 2] << 16) |
                        ((uint32_t)b[4 * q + 3] << 24);
   }
-  // SimView::wsr: workshop k's recipes in dict order, kWsSlots slots per kind (none past that)
-  std::vector<uint4> wsr((size_t)CRAFT_MAX_KINDS * craft::kWsSlots, make_uint4(0, 0, 0, 0));
+  // SimView::wsr: workshop k's recipes in dict order, compact, kWsSlots slots per kind (the
+  // fourth of each kind's 4 stays zero)
+  std::vector<uint2> wsr((size_t)CRAFT_MAX_KINDS * 4, make_uint2(0, 0));
   bool wsr_ok = true;
   {
     int used[CRAFT_MAX_KINDS] = {};
     for (int r = 0; r < cfg->n_recipes; ++r) {
-      const int k = cfg->recipe[r].workshop;
-      if (k <= 0 || k >= CRAFT_MAX_KINDS || used[k] >= craft::kWsSlots) {
+      const craft_recipe_t& rc = cfg->recipe[r];
+      const int k = rc.workshop;
+      if (k <= 0 || k >= CRAFT_MAX_KINDS || used[k] >= craft::kWsSlots || rc.n_inputs > 2) {
         wsr_ok = false;
         continue;
       }
-      wsr[(size_t)k * craft::kWsSlots + used[k]++] = make_uint4(rcw[3 * r], rcw[3 * r + 1], rcw[3 * r + 2], 0u);
+      const uint32_t k0 = rc.n_inputs > 0 ? (uint32_t)rc.input_kind[0] : 0u, c0 = rc.n_inputs > 0 ? (uint32_t)rc.input_count[0] : 0u;
+      const uint32_t k1 = rc.n_inputs > 1 ? (uint32_t)rc.input_kind[1] : 0u, c1 = rc.n_inputs > 1 ? (uint32_t)rc.input_count[1] : 0u;
+      wsr[(size_t)k * 4 + used[k]++] = make_uint2((uint32_t)rc.output | ((uint32_t)k << 8) | (k0 << 16) | (k1 << 24),
+                                                  c0 | (c1 << 8) | ((uint32_t)rc.yield << 16));
     }
   }
   std::vector<uint16_t> task_tab(CRAFT_MAX_TASKS, 0);
@@ -485,7 +489,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
   ALLOC(s->d_mask, 2 * sizeof(uint4) * n_envs);
   ALLOC(s->d_task, sizeof(uint16_t) * task_tab.size());
   ALLOC(s->d_rcw, sizeof(rcw));
-  if (wsr_ok) ALLOC(s->d_wsr, sizeof(uint4) * wsr.size());
+  if (wsr_ok) ALLOC(s->d_wsr, sizeof(uint2) * wsr.size());
   ALLOC(s->d_task_sub, sizeof(int32_t) * task_sub.size());
   ALLOC(s->d_hint, hint_bytes);
   ALLOC(s->d_stats, 4 * sizeof(int64_t) * s->n_tiles);
@@ -519,7 +523,7 @@ int craft_sim_create(const craft_config_t* cfg, int device, int64_t n_envs, int6
     return cleanup(e, "task table");
   if ((e = hipMemcpy(s->d_rcw, rcw, sizeof(rcw), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "recipe table");
-  if (s->d_wsr && (e = hipMemcpy(s->d_wsr, wsr.data(), sizeof(uint4) * wsr.size(), hipMemcpyHostToDevice)) != hipSuccess)
+  if (s->d_wsr && (e = hipMemcpy(s->d_wsr, wsr.data(), sizeof(uint2) * wsr.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "workshop recipe table");
   if ((e = hipMemcpy(s->d_task_sub, task_sub.data(), sizeof(int32_t) * task_sub.size(), hipMemcpyHostToDevice)) != hipSuccess)
     return cleanup(e, "subtask table");
@@ -871,18 +875,16 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   const int nw = craft::teach_words(s->view.W, s->view.H);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
-  // Teacher-table reads in the fused kernel: one L2 line per pristine env.  They hit the
-  // Infinity Cache when the launch rewrites the previous launch's observation buffer (a trainer's
-  // loop: ring 1, -2.5 us per tick) and go to HBM beside the store stream when every launch
-  // writes a fresh buffer (a 16-slot ring: +0.5 us), so auto mode reads them only in the first
-  // case (profiles/r04/ab5).
+  // Teacher-table reads in the fused kernel (its 4-bit copy since round 5): -2.5 us per tick when
+  // the launch rewrites the previous launch's observation buffer (a trainer's loop, ring 1), and
+  // -0.9 us (30.1 -> 29.2) when every launch writes a fresh slot of a 16-slot ring (round 6,
+  // profiles/r06/teach_table_k1; round 4's u16 reads cost +0.5 us there), so auto reads it always.
   {
     const int frc = flush_table(s, stream, "craft_step_teach");
     if (frc != CRAFT_OK) return frc;
   }
   SimView v = teach_view(s);
-  v.tt_fused = s->teach_table == 1 || (s->teach_table == 0 && (a.obs == nullptr || a.obs == s->last_teach_obs));
-  s->last_teach_obs = a.obs;
+  v.tt_fused = s->teach_table != 2;
   if (kernel == 2) {
     e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, nw, s->view.GS, s->view.F), st);
   } else {

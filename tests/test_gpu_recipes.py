@@ -58,12 +58,25 @@ def _same_state(a, b, what):
         assert torch.equal(sa[k].cpu(), sb[k].cpu()), (what, k)
 
 
-@pytest.mark.parametrize("n", [35, 4099])                # tail tiles of 3 envs (32- and 64-env tiles)
-def test_long_recipe_table_every_kernel(n):
-    assert len(long_recipes()["recipes"]) == 13
+def chained_recipes():
+    """Still three recipes per workshop with at most two ingredients (the compact per-workshop
+    table, SimView::wsr), but with an output that is also its own ingredient (stick) and a
+    recipe whose ingredient an earlier one at the same workshop makes (axe from plank)."""
+    r = copy.deepcopy(gamedef.RECIPES)
+    r["recipes"]["stick"] = {"wood": 1, "stick": 1, "_at": "workshop1", "_yield": 3}
+    r["recipes"]["axe"] = {"plank": 1, "iron": 1, "_at": "workshop0"}
+    return r
+
+
+@pytest.mark.parametrize("recipes,n", [("long", 35), ("long", 4099), ("chained", 4099)])
+def test_long_recipe_table_every_kernel(recipes, n):
+    """(long: a workshop with four recipes, which the compact table cannot hold: every kernel's
+    general recipe loop; chained: the compact table's two-round-trip path with its forwarding)"""
+    recipes = long_recipes() if recipes == "long" else chained_recipes()
+    assert len(recipes["recipes"]) in (13, 9)
     params, cb, tm, cfg = make_tables(WORLD)
     pool, _, _ = sample_scenarios(params, cb, 123, 64)
-    g, c = _sims(n, pool, long_recipes())
+    g, c = _sims(n, pool, recipes)
     T = 24
     acts = np.random.RandomState(3).choice(6, size=(T, n), p=[.14, .14, .14, .14, .42, .02]).astype(np.int32)
     # one tick per launch (tile kernel), with the teacher (one-tile or two-tile kernel)
@@ -72,8 +85,9 @@ def test_long_recipe_table_every_kernel(n):
         for s in (g, c):
             s.step(torch.as_tensor(acts[t], device=s.device), tick=t, autoreset=True)
     _same_state(g, c, "step")
-    crafted = g.get_state()["inventory"].cpu().numpy()[:, 21:].sum()
-    assert crafted > 0                                    # the added recipes fired
+    if len(recipes["recipes"]) == 13:
+        crafted = g.get_state()["inventory"].cpu().numpy()[:, 21:].sum()
+        assert crafted > 0                                # the added recipes fired
     _start((g, c), pool, n, 2)
     lab = [torch.empty(n, dtype=torch.int32, device=s.device) for s in (g, c)]
     for t in range(T):
