@@ -39,7 +39,7 @@ constexpr int kTick2Tile = 64;          // envs per tile (one lane each in A + C
 // observation rows [nbuf waves][up16(64/TW*F)] (nbuf: the tick waves, plus the teacher waves
 // when they join D + E, tick2_share)
 struct Tick2Lds {
-  int inv, agent, tinfo, task, tsub, rc, work, obs, bytes;
+  int inv, agent, tinfo, task, tsub, rc, wsr, work, obs, bytes;
 };
 // Whether the teacher waves take D + E chunks once their teaching is done (rows of their own):
 // pairs (2 teacher waves per tile) and grids up to 12x12, where the rows still leave two
@@ -55,7 +55,8 @@ __host__ __device__ inline Tick2Lds tick2_lds(int J, int TW, int GS, int F, int 
   l.task = l.tinfo + n * 4;
   l.tsub = up16(l.task + CRAFT_MAX_TASKS * 2);
   l.rc = l.tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4;
-  l.work = up16(l.rc + CRAFT_MAX_RECIPES * 12);   // deferred BFS list [n] + {count, arrivals, chunk}
+  l.wsr = up16(l.rc + CRAFT_MAX_RECIPES * 12);    // SimView::wsr [CRAFT_MAX_KINDS][4] uint2
+  l.work = l.wsr + CRAFT_MAX_KINDS * 4 * 8;       // deferred BFS list [n] + {count, arrivals, chunk}
   l.obs = up16(l.work + n * 4 + 12);
   l.bytes = l.obs + nbuf * up16(kTick2Tile / TW * F);
   return l;
@@ -84,6 +85,7 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
+  uint2* s_wsr = reinterpret_cast<uint2*>(smem + lay.wsr);
   uint32_t* s_work = reinterpret_cast<uint32_t*>(smem + lay.work);       // deferred BFS queries
   uint32_t* s_wctl = s_work + J * kTick2Tile;                  // {count, teacher arrivals, D + E chunks}
   const int obs_w = (kTick2Sub * F + 15) & ~15;
@@ -151,6 +153,11 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
     for (int q = 0; q < CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS / 64; ++q) sw[q] = TL > 0 ? v.task_sub[lane + 64 * q] : 0;
     if (lane < v.n_tasks) s_task[lane] = (uint16_t)tw;
     if (lane < CRAFT_MAX_RECIPES * 3) s_rc[lane] = rw;
+    if (v.wsr) {                                                          // (each A + C wave its own copy)
+      const uint2 ww0 = v.wsr[lane], ww1 = v.wsr[lane + 64];
+      s_wsr[lane] = ww0;
+      s_wsr[lane + 64] = ww1;
+    }
     if (j == 0 && lane < 3) s_wctl[lane] = 0u;                            // (before the barrier)
     if (TL > 0) {
 #pragma unroll
@@ -254,7 +261,8 @@ __global__ __launch_bounds__(64 * TW + J * kTick2Tile * TL, CRAFT_T2_WPE) void t
           latch_error(v.err, CRAFT_EBADACTION, slot);
         } else {
           const int ox = s.x, oy = s.y;
-          transition<true>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw, slot);
+          if (v.wsr) transition<true, true>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw, slot, s_wsr);
+          else transition<true>(v, s_rc, g, iv, s, m, act, inv_changed, mask_changed, rw, slot);
           code = transition_code(ox, oy, s, inv_changed);
         }
       }
