@@ -10,7 +10,7 @@ import sys
 
 ORDER = ["driver", "steps512", "k1", "k1_ring1", "config5", "config5_k20", "config5_k1", "config5_label",
          "config5_mix", "trainer", "w5",
-         "w5_k1", "config5_w5"]
+         "w5_k1", "config5_w5", "config5_w5_k1"]
 WHAT = {
     "driver": "driver's command (`--steps 20 --warmup 5`)",
     "steps512": "`--steps 512` (32-tick launches)",
@@ -25,6 +25,7 @@ WHAT = {
     "w5": "w = 5 rollout, 20 ticks",
     "w5_k1": "w = 5, one tick per launch",
     "config5_w5": "config 5 at w = 5, K = 20",
+    "config5_w5_k1": "config 5 at w = 5, one `craft_step_teach` per tick",
 }
 
 
