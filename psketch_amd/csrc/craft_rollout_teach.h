@@ -74,10 +74,10 @@ constexpr uint32_t kRtSpinCap = 1u << 22;
 // words [16][3] | control words [8] | label rows [8][4 + TILE] | BFS job queue [32][2 NW + 1] |
 // table requests [4][TILE] | their rows [4] | clearable cells [TILE][2] | hint table:
 // descriptors [64][4], leaf bytes [2048] | nibble positions [4][TILE] | workshop recipes
-// [CRAFT_MAX_KINDS][4] uint2 (SimView::wsr)
+// [CRAFT_MAX_KINDS][4] uint2 (SimView::wsr) | the transition wave's labels [2][TILE]
 struct RtLds {
   int grid, pristine, obs, inv, agent, tinfo, cout, task, tsub, rc, ctrl, rows, jobs, treq, tval, tpend, tcell, hint,
-      tnib, wsr, bytes;
+      tnib, wsr, clab, bytes;
 };
 __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   auto up16 = [](int x) { return (x + 15) & ~15; };
@@ -102,7 +102,8 @@ __host__ __device__ inline RtLds rt_lds(int tile, int GS, int F, int NW) {
   l.hint = up16(l.tcell + tile * 8);                       // craft_host.h hint_tables
   l.tnib = l.hint + CRAFT_MAX_TASKS * 16 + craft_host::kHintLeafCap;   // [kRtLag][tile] nibble in the word
   l.wsr = up16(l.tnib + kRtLag * tile);
-  l.bytes = l.wsr + CRAFT_MAX_KINDS * 4 * 8;
+  l.clab = l.wsr + CRAFT_MAX_KINDS * 4 * 8;               // [2][tile] the transition wave's labels
+  l.bytes = l.clab + 2 * tile * 4;
   return l;
 }
 // envs per tile: 32 for 3x3 windows (as the split rollout kernel), 16 for wider ones (their
@@ -132,6 +133,11 @@ __device__ __forceinline__ int64_t rt_where(uint32_t wait, uint32_t item, uint32
   return (int64_t)(((uint64_t)wait << 60) | ((uint64_t)(item & 0xfffffffu) << 32) | state);
 }
 
+// Set bits of a wave mask below this lane (v_mbcnt).
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Job meta word: band start cell p0 (bits 0-7), dir (8-9), connected (10), label row (11-14),
 // env in the tile (15-20).
 __device__ __forceinline__ uint32_t rt_job_meta(int p0, int d0, int conn, int row, int env) {
@@ -148,7 +154,10 @@ __device__ __forceinline__ int rbyte(const uint32_t (&r)[8], int k) {
   const uint32_t q0 = (k & 8) ? p1 : p0, q1 = (k & 8) ? p3 : p2;
   return (int)((k & 16) ? q1 : q0);
 }
-template <int WIN, int TILE, int NW>
+// LA: the launch's every env acts on its label (label_actions): the transition wave publishes the
+// labels it decodes and the teacher wave takes them instead of walking (a separate instantiation,
+// so that the other launches keep their register allocation: the shared VGPR budget is tight).
+template <int WIN, int TILE, int NW, bool LA>
 __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v, RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int NT = kRtThreads, NWAVE = NT / 64, TW = NWAVE - 1;   // the teacher is the last wave
@@ -181,10 +190,14 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
   int32_t* s_tsub = reinterpret_cast<int32_t*>(smem + lay.tsub);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   uint2* s_wsr = reinterpret_cast<uint2*>(smem + lay.wsr);               // SimView::wsr (when set)
+  // (label actions) item g's labels as the transition wave decoded them: [g & 1][TILE], 0x100 |
+  // label, or 0 where it has none (a BFS answer: the teacher's own walk)
+  uint32_t* s_clab = reinterpret_cast<uint32_t*>(smem + lay.clab);
   const uint4* s_hdesc = reinterpret_cast<const uint4*>(smem + lay.hint);   // [task]: predicates, leaf offset
   const uint8_t* s_hleaf = smem + lay.hint + CRAFT_MAX_TASKS * 16;
   // [0] the claimed unit, [1] barrier arrivals, [2] items whose labels are complete (label actions),
-  // [3] barriers the teacher has arrived at, [4] unused
+  // [3] barriers the teacher has arrived at, [4] items whose labels the transition wave has
+  // published in s_clab (label actions)
   uint32_t* s_ctrl = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
   uint32_t* s_rows = reinterpret_cast<uint32_t*>(smem + lay.rows);    // [8][RW]: ctrl, tag = g + 1, tile, ring slot, labels
   uint32_t* s_jobs = reinterpret_cast<uint32_t*>(smem + lay.jobs);    // [32][JW]
@@ -484,6 +497,14 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
         } else {
           clab = (int)(int8_t)(c_tag & 0xffu);
         }
+      }
+      // (every env on its label) item g - 1's labels published for the teacher wave, which then
+      // needs no walk of its own for them: before the wait below, which waits for the teacher
+      if (LA && k > 0 && lmode == 2 && a.label_actions) {
+        if (lane < TILE)
+          s_clab[((g - 1) & 1) * TILE + lane] = (live && !use_row) ? 0x100u | ((uint32_t)clab & 0xffu) : 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&s_ctrl[4], g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       // mode 1: the row complete; mode 2: the row's BFS answers in (after its walk: s_ctrl[2])
       if (k > 0 && __ballot(live && lsrc && use_row)) {
@@ -866,7 +887,11 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       if (avail == 0) return;
       const uint64_t idle = __ballot(q.ph == kQIdle && ql == 0);
       if (!idle) return;
-      const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
+      // idle quads below this lane's quad (LA: v_mbcnt at the quad's first lane, broadcast to the
+      // quad: no per-lane 64-bit mask, which hipcc keeps live for the whole kernel and spilled there)
+      uint32_t rank;
+      if constexpr (LA) rank = (uint32_t)__builtin_amdgcn_mov_dpp((int)lane_rank(idle), 0x00, 0xf, 0xf, false);
+      else rank = (uint32_t)__popcll(idle & ((1ull << (lane & ~3)) - 1ull));
       const uint32_t taken = min(avail, (uint32_t)__popcll(idle));
       if (q.ph == kQIdle && rank < avail) {
         const uint32_t* J = s_jobs + ((jhead + rank) % kRtQueue) * JW;
@@ -1020,7 +1045,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
     auto push_jobs = [&](uint64_t mask, bool mine, const uint8_t* row8, int kind, int p0, int d0, int cn,
                          int row) __attribute__((always_inline)) {
       if (mine) {
-        const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        const uint32_t rank = LA ? lane_rank(mask) : (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         uint32_t* J = s_jobs + ((jtail + rank) % kRtQueue) * JW;
         const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         Bits<NW> occ, tgt;
@@ -1088,7 +1113,20 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           w_need = 0;                                                  // 1: a table answer, 2: a BFS job
           uint32_t req = ~0u;                                          // (policy actions) the ttab index asked
           uint32_t w_nib = 0;                                          // (nibble table) the nibble in that word
-          if (lane < nE) {
+          // (every env on its label) the transition wave decoded this item's labels at the start
+          // of its next tick (all but BFS answers): taken as they are, no walk for those lanes
+          uint32_t clw = 0;
+          if (LA && lmode == 2 && a.label_actions && i + 1 < nq) {
+            if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_ctrl[4], __ATOMIC_ACQUIRE,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) < g + 1) {
+              wait = true;
+              break;
+            }
+            clw = lane < TILE ? s_clab[(g & 1) * TILE + lane] : 0u;
+          }
+          if (lane < nE && (clw & 0x100u)) {
+            w_label = (int)(int8_t)(clw & 0xffu);
+          } else if (lane < nE) {
             // the walk's loads in three rounds, each issued together: the agent and task words and
             // the row's listed clearable cells; the facing cell, the hint descriptor, the inventory
             // and the listed cells' kinds now; the hint leaf

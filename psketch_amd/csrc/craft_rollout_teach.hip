@@ -6,7 +6,7 @@
 
 namespace craft {
 
-template <int WIN, int NW>
+template <int WIN, int NW, bool LA>
 static hipError_t launch_rt_one(const SimView& v, const RolloutArgs& a, hipStream_t st) {
   constexpr int TILE = rt_tile(WIN);
   const int64_t tiles = (v.n_envs + TILE - 1) / TILE;
@@ -16,14 +16,14 @@ static hipError_t launch_rt_one(const SimView& v, const RolloutArgs& a, hipStrea
 #else
   const size_t lds = (size_t)rt_lds(TILE, v.GS, v.F, NW).bytes;
 #endif
-  auto kern = rollout_teach_kernel<WIN, TILE, NW>;
+  auto kern = rollout_teach_kernel<WIN, TILE, NW, LA>;
   {
-    const hipError_t e = ensure_lds<&rollout_teach_kernel<WIN, TILE, NW>>(lds);
+    const hipError_t e = ensure_lds<&rollout_teach_kernel<WIN, TILE, NW, LA>>(lds);
     if (e != hipSuccess) return e;
   }
   // persistent workgroups: what the chip holds at once, spread so that every workgroup runs the
   // same number of tiles
-  const int resident = resident_workgroups<&rollout_teach_kernel<WIN, TILE, NW>>(kRtThreads, lds);
+  const int resident = resident_workgroups<&rollout_teach_kernel<WIN, TILE, NW, LA>>(kRtThreads, lds);
   const int64_t rounds = (tiles + resident - 1) / resident;
   const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;   // stats_part rows
   const int64_t grid = std::min<int64_t>((tiles + rounds - 1) / rounds, rows);
@@ -32,13 +32,20 @@ static hipError_t launch_rt_one(const SimView& v, const RolloutArgs& a, hipStrea
   return hipGetLastError();
 }
 
-template <int WIN>
-static hipError_t launch_rt_win(int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
+template <int WIN, bool LA>
+static hipError_t launch_rt_nw(int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
   // nw = 32-bit words per BFS cell set (the band of columns 1 .. W-2): 8x8 -> 2, 10x10 -> 3 (run
   // as 4), 12x12 -> 4, up to 15x15 -> 7 (run as 8)
-  if (nw <= 2) return launch_rt_one<WIN, 2>(v, a, st);
-  if (nw <= 4) return launch_rt_one<WIN, 4>(v, a, st);
-  return launch_rt_one<WIN, 8>(v, a, st);
+  if (nw <= 2) return launch_rt_one<WIN, 2, LA>(v, a, st);
+  if (nw <= 4) return launch_rt_one<WIN, 4, LA>(v, a, st);
+  return launch_rt_one<WIN, 8, LA>(v, a, st);
+}
+
+template <int WIN>
+static hipError_t launch_rt_win(int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
+  // every env on its label, the transition wave looking the labels up (lsync 2): the LA kernel
+  if (a.label_actions && a.lsync == 2) return launch_rt_nw<WIN, true>(nw, v, a, st);
+  return launch_rt_nw<WIN, false>(nw, v, a, st);
 }
 
 hipError_t launch_rollout_teach(int win, int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {

@@ -68,11 +68,19 @@ def chained_recipes():
     return r
 
 
-@pytest.mark.parametrize("recipes,n", [("long", 35), ("long", 4099), ("chained", 4099)])
+def triple_recipes():
+    """A recipe with three ingredients, which the compact table cannot hold either."""
+    r = copy.deepcopy(gamedef.RECIPES)
+    r["recipes"]["bed"] = {"plank": 1, "grass": 1, "stick": 1, "_at": "workshop1"}
+    return r
+
+
+@pytest.mark.parametrize("recipes,n", [("long", 35), ("long", 4099), ("chained", 4099), ("triple", 4099)])
 def test_long_recipe_table_every_kernel(recipes, n):
-    """(long: a workshop with four recipes, which the compact table cannot hold: every kernel's
-    general recipe loop; chained: the compact table's two-round-trip path with its forwarding)"""
-    recipes = long_recipes() if recipes == "long" else chained_recipes()
+    """(long: a workshop with four recipes, triple: a recipe with three ingredients, which the
+    compact table cannot hold: every kernel's general recipe loop; chained: the compact table's
+    two-round-trip path with its forwarding)"""
+    recipes = {"long": long_recipes, "chained": chained_recipes, "triple": triple_recipes}[recipes]()
     assert len(recipes["recipes"]) in (13, 9)
     params, cb, tm, cfg = make_tables(WORLD)
     pool, _, _ = sample_scenarios(params, cb, 123, 64)
