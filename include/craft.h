@@ -179,8 +179,9 @@ int craft_sim_tune_rollout(craft_sim_t* sim, int32_t chunk_ticks, int32_t thread
  * craft_sim_tune, replacing nothing in the reference):
  *   kernel  which kernel craft_step_teach launches: 0 (default) = the measured best (the two-tile
  *           kernel with 2 teacher lanes per env for 3x3 windows at >= 32768 envs, else the
- *           one-tile kernel with 4), 1 = the one-tile kernel, 2 = the two-tile kernel (3x3
- *           windows and the default tile only; otherwise the one-tile kernel);
+ *           one-tile kernel: 64-env tiles with 4 lanes for 3x3 windows, the handle's tile (32
+ *           by default) with 2 for wider ones), 1 = the one-tile kernel, 2 = the two-tile
+ *           kernel (3x3 windows and the default tile only; otherwise the one-tile kernel);
  *   lanes   teacher lanes per query: 0 (default) = each kernel's measured best; 1, 2 or 4 for
  *           craft_teacher and the one-tile kernel, 2 or 4 for the two-tile kernel (others: 2);
  *   table   which teachers read the teacher table (find_closest_resources answered ahead of

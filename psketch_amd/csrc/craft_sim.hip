@@ -24,7 +24,7 @@ hipError_t launch_distances(int nw, const SimView& v, const int32_t* tasks, cons
 hipError_t launch_rollout(int win, int tile, int threads, const SimView& v, const RolloutArgs& a, size_t lds,
                           hipStream_t st);
 hipError_t launch_scenarios(const SimView& v, const ScenarioArgs& a, hipStream_t st);
-hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
+hipError_t launch_tick_teach(int tl, int nw, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
                              hipStream_t st);
 hipError_t launch_tick2(int tl, int nw, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st);
 size_t tick2_lds_bytes(int tl, int nw, int GS, int F);
@@ -258,6 +258,12 @@ void rollout_shape(const craft_sim* s, int* tile, int* threads, int* split) {
   *split = (t <= 32 && nt >= 320) ? 1 : 0;
 }
 
+// The one-tile teacher kernel's envs per tile: 64 for 3x3 windows; the handle's tile (default 32)
+// for wider ones, whose 64-env observation rows (69 KB at 5x5) leave one workgroup per CU.
+int teach_tile(const craft_sim* s) {
+  return s->cfg.window_width == 3 || s->tile != 32 ? craft::kMaxTileEnvs : 32;
+}
+
 // What craft_step / craft_step_ex (teach = false) or craft_step_teach (teach = true) launches:
 // CRAFT_KERNEL_TILE (craft_tile.h) or CRAFT_KERNEL_TICK2 (craft_tick2.h), with its envs per
 // tile / workgroup and teacher lanes per env.
@@ -277,9 +283,11 @@ void step_shape(const craft_sim* s, bool teach, int* kernel, int* envs, int* lan
   // teacher lanes per env (craft_sim_tune_teach): the two-tile kernel runs pairs (or quads), the
   // one-tile kernel quads (or pairs, or one lane)
   const int tl2 = s->teach_lanes == 4 ? 4 : 2;
-  const int tl1 = (s->teach_lanes == 1 || s->teach_lanes == 2) ? s->teach_lanes : 4;
+  // (the 32-env tile of wider windows: pairs by default, 76.5 against 78.5 us with quads at 5x5)
+  const int tl1 = (s->teach_lanes == 1 || s->teach_lanes == 2) ? s->teach_lanes
+                  : s->teach_lanes == 0 && teach_tile(s) == 32 ? 2 : 4;
   if (k == 2) { *kernel = 2; *envs = 128; *lanes = tl2; }
-  else { *kernel = 1; *envs = craft::kMaxTileEnvs; *lanes = tl1; }
+  else { *kernel = 1; *envs = teach_tile(s); *lanes = tl1; }
 }
 
 // Builds the teacher-table entries (and listed clearable cells) of the rows loaded since the last
@@ -888,11 +896,11 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
   if (kernel == 2) {
     e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, nw, s->view.GS, s->view.F), st);
   } else {
-    const int tile = craft::kMaxTileEnvs;
+    const int tile = teach_tile(s);
     const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
                        CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16 + tile * 4;
     // + task | frozen words, task_sub, D sync and the deferred-BFS controls, the deferred list
-    e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, v, a, lds, st);
+    e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, tile, v, a, lds, st);
   }
   if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");
   return CRAFT_OK;

@@ -10,12 +10,11 @@
 
 namespace craft {
 
-template <int WIN, int TL, int NW>
+template <int WIN, int TL, int NW, int TILE>
 static hipError_t launch_tt(const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
-  constexpr int TILE = kMaxTileEnvs;
   const int64_t tiles = (a.n + TILE - 1) / TILE;
   if (tiles == 0) return hipSuccess;
-  // 5x5 / 7x7 windows: 64-env rows past 64 KiB
+  // 5x5 / 7x7 windows, 64-env tiles: rows past 64 KiB
   const hipError_t e = ensure_lds<&tile_kernel<WIN, MODE_TICK, TILE, TL, NW>>(lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((tile_kernel<WIN, MODE_TICK, TILE, TL, NW>), dim3((unsigned)tiles),
@@ -23,32 +22,33 @@ static hipError_t launch_tt(const SimView& v, const TileArgs& a, size_t lds, hip
   return hipGetLastError();
 }
 
+// 3x3 windows: 64-env tiles; wider ones 32 (the handle's default tile) or 64
 template <int TL, int NW>
-static hipError_t launch_tt_win(int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+static hipError_t launch_tt_win(int win, int tile, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
   switch (win) {
-    case 3: return launch_tt<3, TL, NW>(v, a, lds, st);
-    case 5: return launch_tt<5, TL, NW>(v, a, lds, st);
-    default: return launch_tt<7, TL, NW>(v, a, lds, st);
+    case 3: return launch_tt<3, TL, NW, kMaxTileEnvs>(v, a, lds, st);
+    case 5: return tile == 32 ? launch_tt<5, TL, NW, 32>(v, a, lds, st) : launch_tt<5, TL, NW, kMaxTileEnvs>(v, a, lds, st);
+    default: return tile == 32 ? launch_tt<7, TL, NW, 32>(v, a, lds, st) : launch_tt<7, TL, NW, kMaxTileEnvs>(v, a, lds, st);
   }
 }
 
 template <int TL>
-static hipError_t launch_tt_nw(int nw, int win, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
+static hipError_t launch_tt_nw(int nw, int win, int tile, const SimView& v, const TileArgs& a, size_t lds, hipStream_t st) {
   // nw = 32-bit words per BFS cell set (craft_teach.h: the band of columns 1 .. W-2):
   // 8x8 -> 2, 10x10 -> 3 (run as 4), 12x12 -> 4, 16x16 -> 7 (run as 8)
-  if (nw <= 2) return launch_tt_win<TL, 2>(win, v, a, lds, st);
-  if (nw <= 4) return launch_tt_win<TL, 4>(win, v, a, lds, st);
-  if (nw <= 5) return launch_tt_win<TL, 5>(win, v, a, lds, st);
-  return launch_tt_win<TL, 8>(win, v, a, lds, st);
+  if (nw <= 2) return launch_tt_win<TL, 2>(win, tile, v, a, lds, st);
+  if (nw <= 4) return launch_tt_win<TL, 4>(win, tile, v, a, lds, st);
+  if (nw <= 5) return launch_tt_win<TL, 5>(win, tile, v, a, lds, st);
+  return launch_tt_win<TL, 8>(win, tile, v, a, lds, st);
 }
 
 // tl = teacher lanes per env: 2 (a pair per env, 2 teacher waves), 4 (a quad, 4 waves) or
 // 1 (one wave).
-hipError_t launch_tick_teach(int tl, int nw, int win, const SimView& v, const TileArgs& a, size_t lds,
+hipError_t launch_tick_teach(int tl, int nw, int win, int tile, const SimView& v, const TileArgs& a, size_t lds,
                              hipStream_t st) {
-  if (tl == 1) return launch_tt_nw<1>(nw, win, v, a, lds, st);
-  if (tl == 4) return launch_tt_nw<4>(nw, win, v, a, lds, st);
-  return launch_tt_nw<2>(nw, win, v, a, lds, st);
+  if (tl == 1) return launch_tt_nw<1>(nw, win, tile, v, a, lds, st);
+  if (tl == 4) return launch_tt_nw<4>(nw, win, tile, v, a, lds, st);
+  return launch_tt_nw<2>(nw, win, tile, v, a, lds, st);
 }
 
 // The two-tile tick kernel (craft_tick2.h) for craft_step_teach, 3x3 windows: 2 or 4 teacher
