@@ -484,7 +484,7 @@ def run(args):
         if K > 1 and teacher:
             tile = 32 if win == 3 else 16
             nw = sim.teach_words()
-            la = "true" if args.teacher_actions == "label" else "false"   # (the label-actions instantiation)
+            la = "true" if args.teacher_actions != "policy" else "false"   # (labels feed actions: the LA instantiation)
             kname = f"rollout_teach_kernel<{win}, {tile}, {nw}, {la}>"
             shape = {"tile": tile, "rollout_threads": 512, "teacher_wave": 1,
                      "rollout_unit_ticks": k_eff, "kernel": "rollout_teach_kernel (craft_rollout_teach)"}

@@ -154,9 +154,10 @@ __device__ __forceinline__ int rbyte(const uint32_t (&r)[8], int k) {
   const uint32_t q0 = (k & 8) ? p1 : p0, q1 = (k & 8) ? p3 : p2;
   return (int)((k & 16) ? q1 : q0);
 }
-// LA: the launch's every env acts on its label (label_actions): the transition wave publishes the
-// labels it decodes and the teacher wave takes them instead of walking (a separate instantiation,
-// so that the other launches keep their register allocation: the shared VGPR budget is tight).
+// LA: labels feed some env's actions (label_actions or behaviour cloning, the transition wave
+// looking them up): it looks every lane's label up, cloning or not, publishes what it decodes,
+// and the teacher wave takes those instead of walking (a separate instantiation, so that the
+// policy launches keep their register allocation: the shared VGPR budget is tight).
 template <int WIN, int TILE, int NW, bool LA>
 __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v, RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -485,24 +486,26 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
       // lookup, or the teacher's row of item g - 1 once complete (the teacher finishes each item
       // inside its interval)
       int clab = 0;
-      bool use_row = false;
-      if (k > 0 && live && lsrc) {
+      bool use_row = false, unknown = false;
+      // (LA: every lane's label is looked up and published, the cloning lanes' and the others')
+      if (k > 0 && live && (lsrc || LA)) {
         if (c_tag & kCNib) {
           const uint32_t code = (c_word >> (4 * (c_tag & 7u))) & 0xfu;
           clab = code < 4 ? (int)code : code == 4 ? CRAFT_STOP : -2;
           if (code > 4)                                                // raises / no entry (as the teacher's decode)
             latch_error(v.err, code == 5 ? CRAFT_ETEACHER : CRAFT_EINVARIANT, slot);
         } else if (c_tag & kCRow) {
-          use_row = true;
+          use_row = lsrc;                                              // (a lane on the policy needs no wait)
+          unknown = true;
         } else {
           clab = (int)(int8_t)(c_tag & 0xffu);
         }
       }
-      // (every env on its label) item g - 1's labels published for the teacher wave, which then
-      // needs no walk of its own for them: before the wait below, which waits for the teacher
-      if (LA && k > 0 && lmode == 2 && a.label_actions) {
+      // (LA) item g - 1's labels published for the teacher wave, which then needs no walk of its
+      // own for them: before the wait below, which waits for the teacher
+      if (LA && k > 0 && lmode == 2) {
         if (lane < TILE)
-          s_clab[((g - 1) & 1) * TILE + lane] = (live && !use_row) ? 0x100u | ((uint32_t)clab & 0xffu) : 0u;
+          s_clab[((g - 1) & 1) * TILE + lane] = (live && !unknown) ? 0x100u | ((uint32_t)clab & 0xffu) : 0u;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_store(&s_ctrl[4], g, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -612,7 +615,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
 #pragma unroll
         for (int i = 0; i < 8; ++i) ivn[i] = reinterpret_cast<const uint32_t*>(iv)[i];
         read_nb(gr);
-        if (lsync && lsrc && k + 1 < a.n_ticks) c_tag = c_label(gr, ivn);
+        if (lsync && (lsrc || LA) && k + 1 < a.n_ticks) c_tag = c_label(gr, ivn);
         // done, success, reward and the recorded action (action_seqs, imitation.py:59-61) leave
         // from the streaming waves, one array each
         s_cout[(k & 1) * TILE + lane] = make_uint2((uint32_t)d | ((uint32_t)(succ + 1) << 1) | ((uint32_t)counted << 3) |
@@ -1116,7 +1119,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           // (every env on its label) the transition wave decoded this item's labels at the start
           // of its next tick (all but BFS answers): taken as they are, no walk for those lanes
           uint32_t clw = 0;
-          if (LA && lmode == 2 && a.label_actions && i + 1 < nq) {
+          if (LA && lmode == 2 && i + 1 < nq) {
             if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_ctrl[4], __ATOMIC_ACQUIRE,
                                                                  __HIP_MEMORY_SCOPE_WORKGROUP)) < g + 1) {
               wait = true;

@@ -43,8 +43,8 @@ static hipError_t launch_rt_nw(int nw, const SimView& v, const RolloutArgs& a, h
 
 template <int WIN>
 static hipError_t launch_rt_win(int nw, const SimView& v, const RolloutArgs& a, hipStream_t st) {
-  // every env on its label, the transition wave looking the labels up (lsync 2): the LA kernel
-  if (a.label_actions && a.lsync == 2) return launch_rt_nw<WIN, true>(nw, v, a, st);
+  // labels feeding actions, the transition wave looking them up (lsync 2): the LA kernel
+  if (a.lsync == 2) return launch_rt_nw<WIN, true>(nw, v, a, st);
   return launch_rt_nw<WIN, false>(nw, v, a, st);
 }
 
