@@ -154,6 +154,7 @@ __device__ __forceinline__ int rbyte(const uint32_t (&r)[8], int k) {
   const uint32_t q0 = (k & 8) ? p1 : p0, q1 = (k & 8) ? p3 : p2;
   return (int)((k & 16) ? q1 : q0);
 }
+
 // LA: labels feed some env's actions (label_actions or behaviour cloning, the transition wave
 // looking them up): it looks every lane's label up, cloning or not, publishes what it decodes,
 // and the teacher wave takes those instead of walking (a separate instantiation, so that the

@@ -430,20 +430,30 @@ def test_rollout_teach_refusals_on_the_gpu():
     sim.check()
 
 
-@pytest.mark.parametrize("n", [1, 7, 33, 95])
-def test_rollout_teach_tiny_batches_equal_cpu_variant(n):
+@pytest.mark.parametrize("n,mode", [(1, "policy"), (7, "policy"), (33, "policy"), (95, "policy"),
+                                    (7, "label"), (33, "label"), (33, "bc"), (95, "bc")])
+def test_rollout_teach_tiny_batches_equal_cpu_variant(n, mode):
     """Fewer envs than one tile, one env past a tile, three tiles minus one: the persistent grid
-    sizes itself to the tiles and the tail tile's idle lanes store nothing."""
+    sizes itself to the tiles and the tail tile's idle lanes store nothing (label / bc: the LA
+    kernel, whose transition wave publishes labels for the tail tile's live lanes only)."""
     world, W, T = "craft_medium_12x12", 12, 30
     cfg, pool, specs = _setup(world, W, n, pool_n=16, seed=n)
     g = sim_with_pool(world, n, pool)
     c = CraftSim(world, n_envs=n, device="cpu", pool_capacity=len(pool))
     c.load_pool(pool)
     outs = []
+    bc = (np.random.RandomState(n).rand(n) < 0.5).astype(np.uint8)
     for s in (g, c):
         s.reset(*specs)
         r = _rings(s, 8)
-        s.rollout_teach(T, seed=4, **r)
+        kw = {}
+        if mode != "policy":
+            kw["label_in"] = s.teacher()[0].clone()
+            if mode == "label":
+                kw["label_actions"] = True
+            else:
+                kw["behavior_clone"] = torch.as_tensor(bc, device=s.device)
+        s.rollout_teach(T, seed=4, autoreset=True, **kw, **r)
         s.check()
         outs.append(({k: v.cpu() for k, v in r.items()}, {k: v.cpu() for k, v in s.get_state().items()}))
     for a, b in zip(*outs):
