@@ -119,9 +119,15 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
           const int k = g[min(max(cx, 0), W - 1) * H + min(max(cy, 0), H - 1)];
           kk[i * WIN + j] = ok ? k : 0;
         }
+      // (a running 32-bit offset: the c * K products hoisted out of the unit loop as 64-bit
+      // pointers held 2 * WIN * WIN registers through every unit)
+      uint32_t off = 0;
 #pragma unroll
-      for (int c = 0; c < WIN * WIN; ++c)
-        if (kk[c]) row[c * K + kk[c]] = 1;
+      for (int c = 0; c < WIN * WIN; ++c) {
+        if (kk[c]) row[off + kk[c]] = 1;
+        off += K;
+        asm volatile("" : "+v"(off));
+      }
       {                                                             // inventory counts
         const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);   // 8 independent reads
         uint32_t w[8];

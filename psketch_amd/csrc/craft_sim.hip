@@ -897,9 +897,10 @@ int craft_step_teach(craft_sim_t* s, const craft_step_args_t* x, int32_t* label_
     e = craft::launch_tick2(tl, nw, v, a, craft::tick2_lds_bytes(tl, nw, s->view.GS, s->view.F), st);
   } else {
     const int tile = teach_tile(s);
-    const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes + tile * 4 +
-                       CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS * 4 + 16 + tile * 4;
-    // + task | frozen words, task_sub, D sync and the deferred-BFS controls, the deferred list
+    // + task_sub as bytes (the teacher's other words live in row padding and the control words,
+    // craft_tile.h): 40,888 bytes for a 32-env tile at 12x12, 5x5, so four workgroups share a CU
+    const size_t lds = (size_t)craft::lds_layout(tile, s->view.GS, s->view.F).bytes +
+                       (((size_t)s->view.n_tasks * CRAFT_MAX_SUBTASKS + 15) & ~size_t(15));
     e = craft::launch_tick_teach(tl, nw, s->cfg.window_width, tile, v, a, lds, st);
   }
   if (e != hipSuccess) return hip_fail(s, e, "craft_step_teach launch");

@@ -632,8 +632,8 @@ __device__ __forceinline__ int hint_leaf(const uint16_t* task_tab, const int32_t
   return -2;
 }
 
-template <int NW, int LANES, bool DEFER = false>
-__device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_tab, const int32_t* task_sub,
+template <int NW, int LANES, bool DEFER = false, typename TS = int32_t>
+__device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_tab, const TS* task_sub,
                                          const uint32_t* row32, const uint32_t (&m)[8],
                                          const uint8_t* iv, const Agent& s, int task, int ql,
                                          bool want_len, int& len_out, int& err_out, bool conn,
@@ -687,7 +687,7 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
     for (int guard = 0; guard < CRAFT_MAX_TASKS; ++guard) {
       const int nsub = (task_tab[node] >> 12) & 0xf;
       if (nsub == 0) break;
-      const int32_t* sub = task_sub + CRAFT_MAX_SUBTASKS * node;
+      const TS* sub = task_sub + CRAFT_MAX_SUBTASKS * node;
       int chosen = sub[nsub - 1];
       bool last = true;
       for (int q = 0; q + 1 < nsub; ++q)
@@ -754,18 +754,20 @@ __device__ __forceinline__ int teach_env(const SimView& v, const uint16_t* task_
 // k < n, answered by the workgroup's teacher lane groups in order (group g takes k = g; every env
 // defers at most one query and there is one group per env, so n <= G), so a wave spends its BFS
 // instructions on envs that need one instead of on the few of its own.  grid / agent / info as the fused kernels keep them in LDS (info: task |
-// frozen << 8 | connected << 9); label: the label row of the workgroup's first env.
+// frozen << 8 | connected << 9); label: the label row of the workgroup's first env; ws / is: the
+// word strides of work and info (1: arrays; the one-tile kernel keeps them in row padding).
 template <int NW, int LANES>
 __device__ __forceinline__ void teach_deferred(const SimView& v, const uint32_t* work, int n, int g, int G, int ql,
                                                const uint8_t* s_grid, int GS, const uint32_t* s_agent,
-                                               const uint32_t* s_info, int32_t* label, int64_t env0) {
+                                               const uint32_t* s_info, int32_t* label, int64_t env0, int ws = 1,
+                                               int is = 1) {
   const int H = v.H, C = v.C, nq = (C + 3) >> 2;
   const Bits<NW> valid = brange<NW>(0, C - 2 * H);
   const uint32_t m0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (g < n) {
-    const uint32_t wk = work[g];
+    const uint32_t wk = work[g * ws];
     const int e = wk & 0xff, kind = (wk >> 8) & 0xff;
-    const uint32_t ag = s_agent[e], ti = s_info[e];
+    const uint32_t ag = s_agent[e], ti = s_info[e * is];
     const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
     Bits<NW> occ, tgt;
     band_bits<NW, LANES>(reinterpret_cast<const uint32_t*>(s_grid + e * GS), nq, C, H, m0, (uint32_t)kind, ql,
@@ -787,11 +789,13 @@ __device__ __forceinline__ void teach_deferred(const SimView& v, const uint32_t*
 template <int NW, int LANES>
 __device__ __forceinline__ void teach_deferred_dense(const SimView& v, const uint32_t* work, int n, int u, int NT,
                                                      const uint8_t* s_grid, int GS, const uint32_t* s_agent,
-                                                     const uint32_t* s_info, int32_t* label, int64_t env0) {
+                                                     const uint32_t* s_info, int32_t* label, int64_t env0,
+                                                     int ws = 1, int is = 1) {
   if (LANES < 4 && n <= NT / 4)
-    teach_deferred<NW, 4>(v, work, n, u >> 2, NT / 4, u & 3, s_grid, GS, s_agent, s_info, label, env0);
+    teach_deferred<NW, 4>(v, work, n, u >> 2, NT / 4, u & 3, s_grid, GS, s_agent, s_info, label, env0, ws, is);
   else
-    teach_deferred<NW, LANES>(v, work, n, u / LANES, NT / LANES, u % LANES, s_grid, GS, s_agent, s_info, label, env0);
+    teach_deferred<NW, LANES>(v, work, n, u / LANES, NT / LANES, u % LANES, s_grid, GS, s_agent, s_info, label, env0,
+                              ws, is);
 }
 
 }  // namespace craft

@@ -18,7 +18,7 @@ static hipError_t launch_tt(const SimView& v, const TileArgs& a, size_t lds, hip
   const hipError_t e = ensure_lds<&tile_kernel<WIN, MODE_TICK, TILE, TL, NW>>(lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((tile_kernel<WIN, MODE_TICK, TILE, TL, NW>), dim3((unsigned)tiles),
-                     dim3(kThreads + TILE * TL), lds, st, v, a);
+                     dim3(tile_tick_threads(TILE, TL) + TILE * TL), lds, st, v, a);
   return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ namespace craft {
 
 // TL > 0 (MODE_TICK only): TILE * TL more threads run the DemonstrationTeacher on
 // every env's new state (craft_step_teach), TL lanes per env, while the first
-// kThreads stream the observations: the BFS reads the grid rows the tick left in
+// tick threads stream the observations: the BFS reads the grid rows the tick left in
 // LDS.  NW = 32-bit words per cell set (teach_env).
 #ifndef CRAFT_TT_WPE
 #define CRAFT_TT_WPE 4
@@ -32,8 +32,15 @@ namespace craft {
 #ifndef CRAFT_TILE_U
 #define CRAFT_TILE_U 4          // 16-byte stores in flight per lane of E
 #endif
+// Tick threads per workgroup (A + C on the first TILE, then D and E on all): 256, or 192 with a
+// teacher on a 32-env tile (craft_step_teach at 5x5 / 7x7), so that with pairs the workgroup is 4
+// waves and four of them share a CU, one wave per SIMD each (the LDS allows four; 5-wave
+// workgroups stopped at three per CU, 70.6 against 60 us for the bare tick at 5x5).
+__host__ __device__ constexpr int tile_tick_threads(int tile, int tl) { return tl > 0 && tile == 32 ? 192 : kThreads; }
+
 template <int WIN, int MODE, int TILE, int TL = 0, int NW = 0>
-__global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) void tile_kernel(SimView v, TileArgs a) {
+__global__ __launch_bounds__(tile_tick_threads(TILE, TL) + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) void tile_kernel(SimView v, TileArgs a) {
+  constexpr int NT = tile_tick_threads(TILE, TL);
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const LdsLayout lay = lds_layout(TILE, v.GS, v.F);
   uint8_t* s_grid = smem;
@@ -42,11 +49,19 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
   uint16_t* s_task = reinterpret_cast<uint16_t*>(smem + lay.task);
   uint32_t* s_rc = reinterpret_cast<uint32_t*>(smem + lay.rc);
   uint32_t* s_agent = reinterpret_cast<uint32_t*>(smem + lay.agent);
-  uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + lay.bytes);   // TL > 0: [TILE] task | frozen << 8
-  int32_t* s_tsub = reinterpret_cast<int32_t*>(s_tinfo + TILE);           // TL > 0: task_sub copy
-  uint32_t* s_dsync = reinterpret_cast<uint32_t*>(s_tsub + CRAFT_MAX_TASKS * CRAFT_MAX_SUBTASKS);   // TL > 0
-  uint32_t* s_wctl = s_dsync + 1;           // TL > 0: {deferred BFS count, teacher arrivals} (craft_teach.h)
-  uint32_t* s_work = s_dsync + 4;           // TL > 0: the deferred BFS queries [TILE]
+  // TL > 0, the teacher's words, packed so that a 32-env tile at 5x5 stays within a quarter of the
+  // CU's LDS (four workgroups per CU, tile_tt_lds_bytes): each env's teacher info word (task |
+  // frozen << 8 | ...) in the 4 pad bytes of its grid row (GS = CS + 4), the deferred BFS
+  // queries in the 4 pad bytes of the inventory rows (counts in the first CRAFT_MAX_KINDS), the
+  // D sync and the deferred-BFS controls in the control words, task_sub as bytes after the layout.
+  static_assert(kInvStride >= CRAFT_MAX_KINDS + 4 && CRAFT_MAX_TASKS <= 127, "teacher words in row padding");
+  uint32_t* s_tinfo = reinterpret_cast<uint32_t*>(smem + v.CS);        // [TILE], word stride GS / 4
+  const int tis = v.GS >> 2;
+  uint32_t* s_work = reinterpret_cast<uint32_t*>(s_inv + CRAFT_MAX_KINDS);   // [TILE], word stride kInvStride / 4
+  constexpr int kWs = kInvStride / 4;
+  uint32_t* s_dsync = reinterpret_cast<uint32_t*>(smem + lay.ctrl);
+  uint32_t* s_wctl = s_dsync + 1;           // {deferred BFS count, teacher arrivals} (craft_teach.h)
+  int8_t* s_tsub = reinterpret_cast<int8_t*>(smem + lay.bytes);        // [n_tasks][CRAFT_MAX_SUBTASKS]
 
   const int tid = threadIdx.x;
   const int64_t env0 = (int64_t)blockIdx.x * TILE;
@@ -116,7 +131,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
     if (TL > 0) {
 #pragma unroll
       for (int q = 0; q < QS; ++q)
-        if (tid + q * TILE < v.n_tasks * CRAFT_MAX_SUBTASKS) s_tsub[tid + q * TILE] = sw[q];
+        if (tid + q * TILE < v.n_tasks * CRAFT_MAX_SUBTASKS) s_tsub[tid + q * TILE] = (int8_t)sw[q];
       if (tid == 0) { *s_dsync = 0u; s_wctl[0] = 0u; s_wctl[1] = 0u; }
     }
     if (live) {
@@ -160,22 +175,30 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
       const uint4* src = reinterpret_cast<const uint4*>(v.pool + (size_t)s.scen * v.CS);
       uint32_t* dst = reinterpret_cast<uint32_t*>(g);
       const int nchunk = v.CS >> 4;
-      uint4 c[CRAFT_MAX_CELLS / 16];
+      // (two batches of up to 8 loads with the teacher waves beside: 32 VGPRs, not 64)
+      constexpr int QB = TL > 0 ? 8 : CRAFT_MAX_CELLS / 16;
 #pragma unroll
-      for (int q = 0; q < CRAFT_MAX_CELLS / 16; ++q)
-        if (q < nchunk) c[q] = src[q];
+      for (int b = 0; b < CRAFT_MAX_CELLS / 16; b += QB) {
+        uint4 c[QB];
 #pragma unroll
-      for (int q = 0; q < CRAFT_MAX_CELLS / 16; ++q)
-        if (q < nchunk) {
-          dst[4 * q + 0] = c[q].x; dst[4 * q + 1] = c[q].y; dst[4 * q + 2] = c[q].z; dst[4 * q + 3] = c[q].w;
-        }
+        for (int q = 0; q < QB; ++q)
+          if (b + q < nchunk) c[q] = src[b + q];
+#pragma unroll
+        for (int q = 0; q < QB; ++q)
+          if (b + q < nchunk) {
+            dst[4 * (b + q) + 0] = c[q].x; dst[4 * (b + q) + 1] = c[q].y;
+            dst[4 * (b + q) + 2] = c[q].z; dst[4 * (b + q) + 3] = c[q].w;
+          }
+      }
     }
     // Every LDS word written above is read below by the same lane, or (the
     // tables) by lanes of this same wave: order the wave's LDS accesses.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifndef CRAFT_STAMPS_TT
     STAMP(1);
+#endif
 
     // ---- C ----
     uint32_t* ivw = reinterpret_cast<uint32_t*>(s_inv + tid * kInvStride);
@@ -293,7 +316,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
 #pragma unroll
       for (int w = 0; w < 8; ++w) ncl += __popc(m[w]);
       const int trow = live ? tt_index(v, s.scen, tcw0, tcw1, ncl, [&](int c) { return g[c] == 0; }) : -1;
-      s_tinfo[tid] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9) |
+      s_tinfo[tid * tis] = (uint32_t)s.task | ((uint32_t)s.frozen << 8) | (conn << 9) |
                      (trow >= 0 ? (1u << 10) | ((uint32_t)trow << 11) : 0u);
     }
     if (MODE == MODE_TICK) {
@@ -310,11 +333,11 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
         if (a.any_live && bl) *a.any_live = 1;          // idempotent plain store
       }
     }
-  } else if (want_obs && tid < kThreads) {
+  } else if (want_obs && tid < NT) {
     // waves 1-3: zero the tile's observation bytes while wave 0 runs A + C
     uint4* z = reinterpret_cast<uint4*>(s_obs);
     const int n16 = (nE * F + 15) >> 4;
-    for (int i = tid - TILE; i < n16; i += kThreads - TILE) z[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid - TILE; i < n16; i += NT - TILE) z[i] = make_uint4(0, 0, 0, 0);
   }
   STAMP(3);
   if (TL == 0 && !want_obs) {
@@ -322,30 +345,32 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
     return;
   }
   __syncthreads();
+#ifndef CRAFT_STAMPS_TT
   STAMP(4);
+#endif
 
   // ---- D: scatter the observation's non-zero bytes ---------------------------------------------
-  if (want_obs && tid < kThreads) scatter_features<WIN, TILE>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
+  if (want_obs && tid < NT) scatter_features<WIN, TILE, NT>(v, s_grid, s_inv, s_agent, s_obs, nE, tid);
   if (TL == 0) {
     if (want_obs) __syncthreads();
-  } else if (want_obs && tid < kThreads) {
+  } else if (want_obs && tid < NT) {
     // D -> E among the tick's 4 waves only (an LDS arrival counter), so the teacher waves
     // start right after C instead of waiting out the scatter at a workgroup barrier
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if ((tid & 63) == 0) __hip_atomic_fetch_add(s_dsync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load(s_dsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)(kThreads / 64))
+    while (__hip_atomic_load(s_dsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)(NT / 64))
       __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
   STAMP(5);
 
-  if constexpr (TL > 0) if (tid >= kThreads) {
+  if constexpr (TL > 0) if (tid >= NT) {
     // ---- T: DemonstrationTeacher on the new state (teachers/demonstration.py:9-30) from the
     // grid row the tick left in LDS (cleared cells already applied), overlapping E ----------
-    const int u = tid - kThreads, e = u / TL, ql = u % TL;
+    const int u = tid - NT, e = u / TL, ql = u % TL;
     if (e < nE) {
       const int64_t i = env0 + e;
-      const uint32_t ag = s_agent[e], ti = s_tinfo[e];
+      const uint32_t ag = s_agent[e], ti = s_tinfo[e * tis];
       int action = -2;                                    // a slot C could not run (error latched)
       if (ag && ((ti >> 8) & 1u)) {
         action = -1;                                      // frozen: the trainer's label for a done env
@@ -366,7 +391,7 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
                                    &defer, (v.tt_fused && ((ti >> 10) & 1u)) ? tt_row4(v, (int)(ti >> 11)) : nullptr);
         if (err && ql == 0) latch_error(v.err, err, i);
         if (action == kTeachDeferred && ql == 0)
-          s_work[__hip_atomic_fetch_add(&s_wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
+          s_work[kWs * __hip_atomic_fetch_add(&s_wctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)] =
               (uint32_t)e | ((uint32_t)defer << 8);
       }
       if (ql == 0 && action != kTeachDeferred) a.label[i] = action;
@@ -378,8 +403,14 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
       __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     const uint32_t nw = __hip_atomic_load(&s_wctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef CRAFT_STAMPS_TT      // diagnostic: 1 the teacher's walks done, 2 its dense pass done, 4 E done
+    if (tid == NT && v.stamps) v.stamps[8 * (int64_t)blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     teach_deferred_dense<NW, TL>(v, s_work, (int)nw, u, TILE * TL, s_grid, v.GS, s_agent, s_tinfo, a.label + env0,
-                                 env0);
+                                 env0, kWs, tis);
+#ifdef CRAFT_STAMPS_TT
+    STAMP_MAX(2);
+#endif
     STAMP_END();
     return;
   }
@@ -390,10 +421,13 @@ __global__ __launch_bounds__(kThreads + TILE * TL, TL > 0 ? CRAFT_TT_WPE : 1) vo
 
   // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
   switch (v.obs_fmt) {
-    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, kThreads, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
-    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, kThreads, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
-    default: stream_obs<CRAFT_OBS_F32, kThreads, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, NT, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, NT, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    default: stream_obs<CRAFT_OBS_F32, NT, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
   }
+#ifdef CRAFT_STAMPS_TT
+  STAMP_MAX(4);
+#endif
   STAMP_END();
 }
 
