@@ -93,7 +93,9 @@ __device__ __forceinline__ void stream_obs(uint8_t* s_obs, void* obs, int64_t en
 //     own block: one read per grid cell (144 at 12x12), not one per block cell (625).
 // (tools/ab.sh: per column is 4 % faster than per block row for w = 5 and 2 % slower
 // for w = 3, where the window holds 81 cells and the masks save writes.)
-template <int WIN, int P>
+// RUN: the local one-hot's writes at a running offset (see below; off for 3x3 windows and in the
+// teacher rollout kernel, whose registers are capped anyway: 973-975 against 981 us there).
+template <int WIN, int P, bool RUN = (WIN > 3)>
 __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t* g, const uint8_t* iv,
                                                  uint32_t ag, uint8_t* row, int part) {
   const int x = ag & 0xff, y = (ag >> 8) & 0xff, dir = (ag >> 16) & 3;
@@ -119,14 +121,21 @@ __device__ __forceinline__ void scatter_env_part(const SimView& v, const uint8_t
           const int k = g[min(max(cx, 0), W - 1) * H + min(max(cy, 0), H - 1)];
           kk[i * WIN + j] = ok ? k : 0;
         }
-      // (a running 32-bit offset: the c * K products hoisted out of the unit loop as 64-bit
-      // pointers held 2 * WIN * WIN registers through every unit)
-      uint32_t off = 0;
+      if constexpr (!RUN) {
 #pragma unroll
-      for (int c = 0; c < WIN * WIN; ++c) {
-        if (kk[c]) row[off + kk[c]] = 1;
-        off += K;
-        asm volatile("" : "+v"(off));
+        for (int c = 0; c < WIN * WIN; ++c)
+          if (kk[c]) row[c * K + kk[c]] = 1;
+      } else {
+        // a running 32-bit offset: at 5x5 / 7x7 the c * K products, hoisted out of the unit loop as
+        // 64-bit pointers, held 2 * WIN * WIN registers through every unit (tile_kernel<5>: 108 -> 95
+        // VGPRs, rollout_kernel<5>: 204 -> 156; 1018-1028 -> 1004-1015 us per 20 ticks)
+        uint32_t off = 0;
+#pragma unroll
+        for (int c = 0; c < WIN * WIN; ++c) {
+          if (kk[c]) row[off + kk[c]] = 1;
+          off += K;
+          asm volatile("" : "+v"(off));
+        }
       }
       {                                                             // inventory counts
         const uint32_t* ivw = reinterpret_cast<const uint32_t*>(iv);   // 8 independent reads

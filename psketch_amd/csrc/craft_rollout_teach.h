@@ -704,7 +704,7 @@ __global__ __launch_bounds__(kRtThreads, 4) void rollout_teach_kernel(SimView v,
           const int e = lane % TILE;
           const uint32_t ag = s_agent[(i & 1) * TILE + e];
           if (e < nE && ((ag >> 24) & 1u))
-            scatter_env_part<WIN, P>(v, s_grid + (i & 1) * TILE * GS + e * GS,
+            scatter_env_part<WIN, P, false>(v, s_grid + (i & 1) * TILE * GS + e * GS,
                                      s_inv + (i & 1) * TILE * kInvStride + e * kInvStride, ag,
                                      s_obs + (i & 1) * obs_buf + e * F, lane / TILE);
         }
