@@ -61,6 +61,47 @@ def test_step_teach_equals_step_then_teacher(world, W, n, T, autoreset, given, k
     b.check()
 
 
+# The one-tile kernel on 32-env tiles (5x5 / 7x7 windows, tile_kernel<WIN, 0, 32, 2, NW>): 192 tick
+# threads beside the teacher pairs, each env's teacher word and the deferred BFS list in row
+# padding, task_sub as bytes (craft_tile.h).  table 2: every go leaf is a deferred BFS, so the
+# list fills; USE raised in the given actions, so cells are cleared and recipes run.
+@pytest.mark.parametrize("world,W,n,T,table,given", [
+    ("craft_medium_12x12_w5", 12, 65536, 10, 0, False),   # config 5's size: four workgroups per CU
+    ("craft_medium_12x12_w5", 12, 5000, 30, 2, True),     # the deferred list full; a partial tile
+    ("craft_large", 10, 4000, 25, 2, True),
+    (dict(WIDTH=12, HEIGHT=12, WINDOW_WIDTH=7, WINDOW_HEIGHT=7, N_WORKSHOPS=3, N_PRIMITIVES=2, N_WORLDS=100),
+     12, 3000, 25, 2, True)])
+def test_step_teach_wide_windows_equal_step_then_teacher(world, W, n, T, table, given):
+    params, cb, tm, cfg = make_tables(world)
+    pool, _, _ = sample_scenarios(params, cb, 123, 256)
+    specs = synthetic_specs(pool, W, W, n, 0, seed=11, task_ids=[t.id for t in tm.dataset_tasks()])
+    a, b = sim_with_pool(world, n, pool), sim_with_pool(world, n, pool)
+    a.tune_teach(1, 0, table)
+    kname, envs, lanes = a.step_shape(teach=True)
+    assert (envs, lanes) == (32, 2), (kname, envs, lanes)
+    a.reset(*specs)
+    b.reset(*specs)
+    F = a.n_features
+    rng = np.random.RandomState(5)
+    oa, ob = (torch.empty((n, F), dtype=torch.float32, device="cuda") for _ in range(2))
+    la = torch.empty(n, dtype=torch.int32, device="cuda")
+    for t in range(T):
+        acts = (torch.as_tensor(rng.choice(6, size=n, p=[.15, .15, .15, .15, .38, .02]).astype(np.int32),
+                                device="cuda") if given else None)
+        a.step(acts, seed=3, tick=t, autoreset=not given, obs=oa, labels=la)
+        b.step(acts, seed=3, tick=t, autoreset=not given, obs=ob)
+        lb, _ = b.teacher()
+        assert torch.equal(oa, ob), t
+        assert torch.equal(la, lb), t
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    if given:                                             # cells were cleared (deferred BFS queries)
+        assert bool((sa["grid"].cpu().numpy() != pool[sa["spec"].cpu().numpy()[:, 0]]).any())
+    a.check()
+    b.check()
+
+
 def test_step_teach_vs_oracle(oracle_mod):
     """The fused labels of 65536 mid-rollout envs against the literal BFS oracle
     on 1024 of them."""
