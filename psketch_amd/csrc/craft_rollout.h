@@ -497,17 +497,9 @@ static hipError_t launch_rollout_split_one(const SimView& v, const RolloutArgs& 
                               : ensure_lds<&rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>>(lds);
     if (e != hipSuccess) return e;
   }
-  static int resident_of[2] = {0, 0};                 // per instantiation (flat or not)
-  static size_t resident_lds[2] = {0, 0};
-  int& resident = resident_of[flat ? 1 : 0];
-  if (resident == 0 || resident_lds[flat ? 1 : 0] != lds) {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NT, lds) != hipSuccess || per_cu < 1) per_cu = 1;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-      cus = 256;
-    resident = per_cu * cus;
-    resident_lds[flat ? 1 : 0] = lds;
-  }
+  // persistent workgroups: what the device holds at once (cached per device and LDS size)
+  const int resident = flat ? resident_workgroups<&rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, kFlatShape>>(NT, lds)
+                            : resident_workgroups<&rollout_split_kernel<WIN, TILE, NT, FMT, WPE, GIVEN, false>>(NT, lds);
   const int64_t units = tiles * (int64_t)((a.n_ticks + a.chunk - 1) / a.chunk);
   const int64_t rounds = (units + resident - 1) / resident;
   const int64_t rows = (v.n_envs + kMinTileEnvs - 1) / kMinTileEnvs;
