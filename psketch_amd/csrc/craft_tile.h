@@ -30,7 +30,12 @@ namespace craft {
 #define CRAFT_TT_WPE 4
 #endif
 #ifndef CRAFT_TILE_U
-#define CRAFT_TILE_U 4          // 16-byte stores in flight per lane of E
+#define CRAFT_TILE_U 4          // 16-byte stores in flight per lane of E (3x3 windows)
+#endif
+// 5x5 / 7x7: 2 (alternating on one box, 32-env tiles at 65,536 envs: the bare tick 61.6 -> 60.9 us,
+// with the teacher 66.1 -> 64.7-65.6; 8 no better than 4)
+#ifndef CRAFT_TILE_U_WIDE
+#define CRAFT_TILE_U_WIDE 2
 #endif
 // Tick threads per workgroup (A + C on the first TILE, then D and E on all): 256, or 192 with a
 // teacher on a 32-env tile (craft_step_teach at 5x5 / 7x7), so that with pairs the workgroup is 4
@@ -420,10 +425,11 @@ __global__ __launch_bounds__(tile_tick_threads(TILE, TL) + TILE * TL, TL > 0 ? C
   }
 
   // ---- E: stream the tile's rows to HBM in the handle's observation format ------------------
+  constexpr int U = WIN == 3 ? CRAFT_TILE_U : CRAFT_TILE_U_WIDE;
   switch (v.obs_fmt) {
-    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, NT, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
-    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, NT, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
-    default: stream_obs<CRAFT_OBS_F32, NT, false, CRAFT_TILE_U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_BF16: stream_obs<CRAFT_OBS_BF16, NT, false, U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    case CRAFT_OBS_U8: stream_obs<CRAFT_OBS_U8, NT, false, U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
+    default: stream_obs<CRAFT_OBS_F32, NT, false, U>(s_obs, a.obs, env0, F, nE, v.obs_policy, tid); break;
   }
 #ifdef CRAFT_STAMPS_TT
   STAMP_MAX(4);
